@@ -1,0 +1,246 @@
+#!/usr/bin/env python3
+"""Headline benchmark: all_reduce busbw + p50 latency, 1 GiB fp32 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]            # N=1 (default)
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N  # N>1
+
+One rank per GPU, backend ``mi355x`` (this library). A "step" is one in-place
+``dist.all_reduce(SUM)`` of a 1 GiB fp32 tensor (268,435,456 synthetic random
+elements per rank). W untimed warm-up steps, then exactly K steps bracketed by
+``barrier + torch.cuda.synchronize()`` on both sides; the time is the MAX over
+ranks. busbw uses the nccl-tests convention ``S * 2(n-1)/n / t`` (0 at n=1,
+where all_reduce is a no-op). p50 = median over K individually-bracketed steps
+of the max-over-ranks time (BASELINE.md method). Rank 0 prints ONE JSON line.
+
+Extra fields (not part of the headline): K1 kernel bandwidth on this GPU, and
+for N>1 an A/B of the algorithms (RCCL vs the IPC peer-memory kernels) at the
+headline size and at small sizes, each with a correctness check.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_BUSBW = {2: 6.14, 4: 5.49, 8: 3.16}  # BASELINE.md §2.1 (reference stack, Gloo/CPU)
+NBYTES = 1 << 30
+
+
+def busbw(nbytes: int, n: int, sec: float) -> float:
+    return 0.0 if n <= 1 or sec <= 0 else nbytes * 2 * (n - 1) / n / sec / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bytes", type=int, default=NBYTES)
+    ap.add_argument("--extras", type=int, default=int(os.environ.get("PDCC_BENCH_EXTRAS", "1")))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import pytorch_distributed_collective_communication_amd as pdcc
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    pdcc._load_native()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            from pytorch_distributed_collective_communication_amd.parallel.spawn import free_port
+
+            os.environ["MASTER_PORT"] = str(free_port())
+    dist.init_process_group("mi355x", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=10))
+    native = be.native_backend()
+
+    numel = args.bytes // 4
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.rand(numel, device=dev, generator=gen).mul_(1e-3)
+
+    def sync():
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)  # CPU tensor: host transport
+        return t.item()
+
+    for _ in range(args.warmup):
+        dist.all_reduce(x)
+    sync()
+    # ---- the timed region: exactly K steps
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    total = max_over_ranks(time.perf_counter() - t0)
+    algo = native.last_algo()
+    ms_per_step = total / args.steps * 1e3
+
+    # ---- p50 of individually bracketed steps (BASELINE.md method)
+    lat = []
+    for _ in range(args.steps):
+        sync()
+        s0 = time.perf_counter()
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        lat.append(max_over_ranks(time.perf_counter() - s0))
+    p50 = statistics.median(lat)
+
+    # ---- correctness of the headline path
+    y = torch.full((numel,), float(rank + 1), device=dev)
+    dist.all_reduce(y)
+    exp = world * (world + 1) / 2
+    correct = bool(torch.all(y == exp).item())
+    del y
+
+    value = busbw(args.bytes, world, ms_per_step / 1e3)
+    extras = {}
+    if args.extras:
+        try:
+            extras = run_extras(world, rank, dev, native, x)
+        except Exception as e:  # extras never break the headline line
+            extras = {"error": f"{type(e).__name__}: {e}"[:500]}
+
+    if rank == 0:
+        line = {
+            "metric": "all_reduce busbw (GB/s) + p50 latency, 1 GiB fp32",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "p50_ms": round(p50 * 1e3, 4),
+            "busbw_p50_GBps": round(busbw(args.bytes, world, p50), 3),
+            "algbw_GBps": round(args.bytes / (ms_per_step / 1e3) / 1e9, 3) if world > 1 else None,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_BUSBW[world], 2) if world in BASELINE_BUSBW else None,
+            "dtype": "fp32",
+            "data": "synthetic (torch.rand, 1 GiB per rank)",
+            "config": {
+                "model": "all_reduce SUM 1 GiB fp32 (reference main.py do_all_reduce, scaled to BASELINE.json)",
+                "global_batch": world,
+                "seq_len": numel,
+                "parallelism": f"dp{world}",
+                "backend": "mi355x",
+                "algo": algo,
+            },
+            "correct": correct,
+            "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+
+
+def _time_op(fn, iters, warm=2):
+    import torch
+    import torch.distributed as dist
+
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def run_extras(world, rank, dev, native, x):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd import ops
+
+    out = {}
+    # K1 on this GPU: 2-source fp32 reduce of 256 MiB per source, LDS-DMA vs register staging
+    n = 64 << 20
+    a = torch.rand(n, device=dev)
+    b = torch.rand(n, device=dev)
+    c = torch.empty_like(a)
+    for impl in ("lds", "regs"):
+        t = _time_op(lambda: ops.reduce_nway([a, b], out=c, impl=impl), 10) if world > 1 else _time_local(
+            lambda: ops.reduce_nway([a, b], out=c, impl=impl), 10)
+        out[f"k1_2src_f32_{impl}_GBps"] = round(3 * n * 4 / t / 1e9, 1)
+    ok = bool(torch.allclose(c, a + b))
+    out["k1_correct"] = ok
+    del a, b, c
+    if world == 1:
+        return out
+
+    # algorithm A/B on a short-timeout subgroup (a stuck peer aborts in 60 s, not 10 min)
+    g = dist.new_group(list(range(world)), timeout=datetime.timedelta(seconds=60))
+    gb = g._get_backend(torch.device("cuda"))
+    flag = torch.ones(1)
+
+    def agree(ok_local: bool) -> bool:
+        f = torch.tensor([1.0 if ok_local else 0.0])
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return f.item() > 0
+
+    for algo in ("rccl", "ipc"):
+        try:
+            gb.set_algo(algo)
+            for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, 1 << 30):
+                t = x[: nbytes // 4]
+                lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
+                out[f"allreduce_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
+                if nbytes >= (1 << 20):
+                    out[f"allreduce_{algo}_{nbytes}B_busbw"] = round(busbw(nbytes, world, lat), 1)
+            v = torch.full((1 << 20,), float(rank + 1), device=dev)
+            dist.all_reduce(v, group=g)
+            good = bool(torch.all(v == world * (world + 1) / 2).item())
+            out[f"allreduce_{algo}_correct"] = good
+        except Exception as e:
+            out[f"allreduce_{algo}_error"] = f"{type(e).__name__}: {e}"[:300]
+            good = False
+        if not agree(good):
+            out["stopped_after"] = algo
+            break
+    try:
+        gb.set_algo("auto")
+    except Exception:
+        pass
+    return out
+
+
+def _time_local(fn, iters):
+    import torch
+
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+if __name__ == "__main__":
+    main()

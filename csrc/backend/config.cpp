@@ -1,0 +1,84 @@
+#include "config.h"
+
+#include <cstdlib>
+#include <sstream>
+#include <stdexcept>
+
+namespace pdcc {
+
+namespace {
+const char* env(const char* k) {
+  const char* v = std::getenv(k);
+  return (v && *v) ? v : nullptr;
+}
+size_t env_size(const char* k, size_t def) {
+  const char* v = env(k);
+  if (!v) return def;
+  char* end = nullptr;
+  double x = std::strtod(v, &end);
+  std::string suf = end ? std::string(end) : "";
+  if (suf == "k" || suf == "K" || suf == "KiB") x *= 1024.0;
+  else if (suf == "m" || suf == "M" || suf == "MiB") x *= 1024.0 * 1024.0;
+  else if (suf == "g" || suf == "G" || suf == "GiB") x *= 1024.0 * 1024.0 * 1024.0;
+  return (size_t)x;
+}
+int env_int(const char* k, int def) {
+  const char* v = env(k);
+  return v ? std::atoi(v) : def;
+}
+bool env_bool(const char* k, bool def) {
+  const char* v = env(k);
+  if (!v) return def;
+  std::string s(v);
+  return !(s == "0" || s == "false" || s == "False" || s == "no" || s == "off");
+}
+}  // namespace
+
+const char* algo_name(Algo a) {
+  switch (a) {
+    case Algo::AUTO: return "auto";
+    case Algo::RCCL: return "rccl";
+    case Algo::IPC: return "ipc";
+    case Algo::HOST: return "host";
+  }
+  return "?";
+}
+
+Config Config::from_env() {
+  Config c;
+  if (const char* a = env("PDCC_ALGO")) {
+    std::string s(a);
+    if (s == "auto") c.force_algo = Algo::AUTO;
+    else if (s == "rccl") c.force_algo = Algo::RCCL;
+    else if (s == "ipc") c.force_algo = Algo::IPC;
+    else if (s == "host") c.force_algo = Algo::HOST;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|ipc|host, got " + s);
+  }
+  c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
+  c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);
+  c.ipc_copy_max = env_size("PDCC_IPC_COPY_MAX", c.ipc_copy_max);
+  c.ipc_max_staging = env_size("PDCC_IPC_MAX_STAGING", c.ipc_max_staging);
+  c.ipc_enable = env_bool("PDCC_IPC", c.ipc_enable);
+  c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
+  c.shm_slot_bytes = env_size("PDCC_SHM_SLOT_BYTES", c.shm_slot_bytes);
+  c.shm_chan_bytes = env_size("PDCC_SHM_CHAN_BYTES", c.shm_chan_bytes);
+  c.debug = env_bool("PDCC_DEBUG", c.debug);
+  c.log_level = env_int("PDCC_LOG_LEVEL", c.log_level);
+  c.blocking_wait = env_bool("PDCC_BLOCKING_WAIT", c.blocking_wait);
+  c.roctx = env_bool("PDCC_ROCTX", c.roctx);
+  c.watchdog_ms = env_int("PDCC_WATCHDOG_MS", c.watchdog_ms);
+  if (const char* f = env("PDCC_FAULT")) c.fault = f;
+  return c;
+}
+
+std::string Config::describe() const {
+  std::ostringstream o;
+  o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_1shot_max=" << ipc_1shot_max
+    << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
+    << " ipc_max_staging=" << ipc_max_staging << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
+    << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
+    << " watchdog_ms=" << watchdog_ms;
+  return o.str();
+}
+
+}  // namespace pdcc

@@ -1,0 +1,40 @@
+// Backend configuration: every knob is a PDCC_* environment variable read once
+// when a process group is constructed. The Python mirror is
+// pytorch_distributed_collective_communication_amd/config.py.
+#pragma once
+#include <chrono>
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace pdcc {
+
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST };
+
+struct Config {
+  // algorithm selection
+  Algo force_algo = Algo::AUTO;            // PDCC_ALGO=auto|rccl|ipc|host
+  size_t ipc_1shot_max = 512u << 10;       // PDCC_IPC_1SHOT_MAX   all-reduce/reduce <= this: 1-shot
+  size_t ipc_2shot_max = 8u << 20;         // PDCC_IPC_2SHOT_MAX   <= this: 2-shot, else RCCL
+  size_t ipc_copy_max = 1u << 20;          // PDCC_IPC_COPY_MAX    broadcast/gather/... <= this: IPC
+  size_t ipc_max_staging = 512u << 20;     // PDCC_IPC_MAX_STAGING per parity; larger messages are chunked
+  bool ipc_enable = true;                  // PDCC_IPC=0 disables the peer-memory path
+  bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
+  // host transport
+  size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES
+  size_t shm_chan_bytes = 1u << 20;        // PDCC_SHM_CHAN_BYTES
+  // robustness / observability
+  bool debug = false;                      // PDCC_DEBUG=1: cross-rank op fingerprint check
+  int log_level = 0;                       // PDCC_LOG_LEVEL 0 quiet, 1 info, 2 every collective
+  bool blocking_wait = false;              // PDCC_BLOCKING_WAIT=1: Work.wait() blocks the host
+  bool roctx = false;                      // PDCC_ROCTX=1: roctx ranges per collective
+  int watchdog_ms = 100;                   // PDCC_WATCHDOG_MS poll period (0 disables)
+  std::string fault;                       // PDCC_FAULT=rank:seq:kind (kind exit|raise|hang)
+
+  static Config from_env();
+  std::string describe() const;
+};
+
+const char* algo_name(Algo a);
+
+}  // namespace pdcc

@@ -1,0 +1,765 @@
+// GPU data paths of ProcessGroupMI355X.
+//
+// Every collective is enqueued on a per-device high-priority comm stream that
+// first waits (hipEvent) for the caller's current stream, exactly like the
+// reference's sync `dist.*` calls appear to the user (main.py:14-83) but without
+// blocking the host. Per call one of three engines runs:
+//   IPC  -- csrc/kernels: stage into own registered buffer, flag peers, pull or
+//           reduce straight from every peer's buffer over xGMI (1-/2-shot)
+//   RCCL -- ncclAllReduce/Reduce/Broadcast/AllGather/ReduceScatter/AllToAll and
+//           grouped ncclSend/Recv (gather/scatter/uneven all-to-all/p2p)
+//   HOST -- D2H, the shared-memory host transport, H2D (fallback only)
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <unistd.h>
+
+#include <cstring>
+
+#include "../device/comm_util.h"
+#include "process_group.h"
+
+namespace pdcc {
+
+namespace {
+
+using RedOpType = c10d::ReduceOp::RedOpType;
+
+bool kern_dtype(at::ScalarType t, kern::DType& d) {
+  switch (t) {
+    case at::kFloat: d = kern::DType::F32; return true;
+    case at::kHalf: d = kern::DType::F16; return true;
+    case at::kBFloat16: d = kern::DType::BF16; return true;
+    case at::kDouble: d = kern::DType::F64; return true;
+    case at::kChar: d = kern::DType::I8; return true;
+    case at::kByte: d = kern::DType::U8; return true;
+    case at::kInt: d = kern::DType::I32; return true;
+    case at::kLong: d = kern::DType::I64; return true;
+    case at::kBool: d = kern::DType::BOOL; return true;
+    default: return false;
+  }
+}
+
+bool kern_op(RedOpType op, kern::RedOp& o) {
+  switch (op) {
+    case RedOpType::SUM: o = kern::RedOp::SUM; return true;
+    case RedOpType::AVG: o = kern::RedOp::AVG; return true;
+    case RedOpType::PRODUCT: o = kern::RedOp::PROD; return true;
+    case RedOpType::MIN: o = kern::RedOp::MIN; return true;
+    case RedOpType::MAX: o = kern::RedOp::MAX; return true;
+    case RedOpType::BAND: o = kern::RedOp::BAND; return true;
+    case RedOpType::BOR: o = kern::RedOp::BOR; return true;
+    case RedOpType::BXOR: o = kern::RedOp::BXOR; return true;
+    default: return false;
+  }
+}
+
+bool nccl_dtype(at::ScalarType t, ncclDataType_t& d) {
+  switch (t) {
+    case at::kFloat: d = ncclFloat32; return true;
+    case at::kHalf: d = ncclFloat16; return true;
+    case at::kBFloat16: d = ncclBfloat16; return true;
+    case at::kDouble: d = ncclFloat64; return true;
+    case at::kChar: d = ncclInt8; return true;
+    case at::kByte: d = ncclUint8; return true;
+    case at::kBool: d = ncclUint8; return true;
+    case at::kInt: d = ncclInt32; return true;
+    case at::kLong: d = ncclInt64; return true;
+    default: return false;
+  }
+}
+
+bool nccl_op(RedOpType op, at::ScalarType t, ncclRedOp_t& o) {
+  const bool b = t == at::kBool;  // bool: SUM = OR = max, PRODUCT = AND = min
+  switch (op) {
+    case RedOpType::SUM: o = b ? ncclMax : ncclSum; return true;
+    case RedOpType::PRODUCT: o = b ? ncclMin : ncclProd; return true;
+    case RedOpType::MIN: o = ncclMin; return true;
+    case RedOpType::MAX: o = ncclMax; return true;
+    case RedOpType::AVG: o = ncclAvg; return !b;
+    default: return false;
+  }
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// input used in place: contiguous + 16-B aligned, else a copy (on the current stream)
+at::Tensor prep_in(const at::Tensor& t) {
+  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
+  at::Tensor c = at::empty_like(t, at::MemoryFormat::Contiguous);
+  c.copy_(t);
+  return c;
+}
+// pure output: contiguous + aligned, else fresh storage (copied back afterwards)
+at::Tensor prep_out(const at::Tensor& t) {
+  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
+  return at::empty_like(t, at::MemoryFormat::Contiguous);
+}
+
+// consecutive views of one allocation, in rank order?
+bool is_flat(const std::vector<at::Tensor>& v, size_t bytes) {
+  if (v.empty()) return false;
+  const char* base = static_cast<const char*>(v[0].data_ptr());
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (!v[i].is_contiguous()) return false;
+    if (static_cast<const char*>(v[i].data_ptr()) != base + i * bytes) return false;
+  }
+  return true;
+}
+
+// K2 (one launch) when every descriptor is 16-B aligned, hipMemcpyAsync otherwise
+void multi_copy_or_memcpy(const std::vector<kern::CopyDesc>& d, hipStream_t s) {
+  bool ok = true;
+  for (const auto& x : d) ok = ok && aligned16(x.src) && aligned16(x.dst);
+  if (ok) {
+    PDCC_HIP(kern::multi_copy(d.data(), (int)d.size(), s));
+  } else {
+    for (const auto& x : d)
+      if (x.bytes) PDCC_HIP(hipMemcpyAsync(x.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, s));
+  }
+}
+
+}  // namespace
+
+// =================================================================== device state
+DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
+  const int d = t.device().index();
+  std::lock_guard<std::mutex> lk(init_mu_);
+  auto it = devs_.find(d);
+  if (it != devs_.end()) return *it->second;
+  TORCH_CHECK(devs_.empty(), "pdcc: one GPU per rank per process group (got a tensor on cuda:", d,
+              " after using cuda:", devs_.begin()->first, ")");
+  c10::hip::HIPGuard g((c10::DeviceIndex)d);
+  char bus[64] = {0};
+  PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
+  char host[256] = {0};
+  gethostname(host, sizeof(host) - 1);
+  const std::string rec = std::string(host) + "|" + bus;
+  const auto all = store_allgather(store_, "pdcc/dev", rank_, size_, std::vector<uint8_t>(rec.begin(), rec.end()));
+  std::vector<std::string> recs;
+  for (const auto& v : all) recs.emplace_back(v.begin(), v.end());
+  bool shared = false;
+  for (int a = 0; a < size_; ++a)
+    for (int b = a + 1; b < size_; ++b) shared = shared || recs[a] == recs[b];
+  bool ok = cfg_.ipc_enable && same_host_ && size_ >= 2 && size_ <= kern::kMaxRanks;
+  for (int r = 0; r < size_ && ok; ++r) {
+    if (recs[r] == rec) continue;
+    const std::string pb = recs[r].substr(recs[r].find('|') + 1);
+    int idx = -1;
+    if (hipDeviceGetByPCIBusId(&idx, pb.c_str()) != hipSuccess) {
+      (void)hipGetLastError();
+      ok = false;
+      break;
+    }
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, d, idx) != hipSuccess || !can) ok = false;
+  }
+  // every rank must agree (a rank that cannot see its peers vetoes the IPC path)
+  const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
+  for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
+
+  auto ds = std::make_unique<DeviceState>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)d));
+  ds->device = d;
+  ds->shared_device = shared;
+  ds->rccl_ok = !shared;
+  ds->ipc_ok = ok;
+  if (cfg_.log_level >= 1)
+    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d shared_device=%d\n", rank_, d, bus,
+            (int)ds->rccl_ok, (int)ds->ipc_ok, (int)shared);
+  DeviceState& ref = *ds;
+  devs_[d] = std::move(ds);
+  return ref;
+}
+
+RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
+  if (!ds.rccl) {
+    auto c = std::make_unique<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device);
+    std::lock_guard<std::mutex> lk(init_mu_);
+    ds.rccl = std::move(c);
+  }
+  return *ds.rccl;
+}
+
+IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
+  if (!ds.ipc) {
+    auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging,
+                                       (uint64_t)timeout_.count(), ds.shared_device);
+    std::lock_guard<std::mutex> lk(init_mu_);
+    ds.ipc = c;
+  }
+  return *ds.ipc;
+}
+
+Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can) {
+  (void)ds;
+  if (cfg_.force_algo == Algo::HOST) return Algo::HOST;
+  if (cfg_.force_algo == Algo::RCCL && rccl_can) return Algo::RCCL;
+  if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
+  if (ipc_can) {
+    size_t lim = cfg_.ipc_copy_max;
+    if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
+    if (bytes <= lim) return Algo::IPC;
+  }
+  if (rccl_can) return Algo::RCCL;
+  if (ipc_can) return Algo::IPC;
+  return Algo::HOST;
+}
+
+void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per_call_max, hipStream_t s) {
+  size_t chunk = per_call_max / kern::kTileBytes * kern::kTileBytes;
+  if (chunk == 0) chunk = kern::kTileBytes;
+  const size_t total = call.bytes;
+  if (total <= chunk) {
+    ic.launch(call, s);
+    return;
+  }
+  for (size_t off = 0; off < total; off += chunk) {
+    kern::IpcCall c = call;
+    c.bytes = std::min(chunk, total - off);
+    for (int k = 0; k < kern::kMaxRanks; ++k) {
+      if (call.in[k]) c.in[k] = static_cast<const char*>(call.in[k]) + off;
+      if (call.out[k]) c.out[k] = static_cast<char*>(call.out[k]) + off;
+    }
+    ic.launch(c, s);
+  }
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& ds,
+                                                           const std::vector<at::Tensor>& keep_alive,
+                                                           std::vector<at::Tensor> outputs,
+                                                           std::chrono::milliseconds timeout,
+                                                           const std::function<void(hipStream_t)>& fn,
+                                                           std::shared_ptr<IpcComm> ipcp) {
+  c10::hip::HIPGuard g((c10::DeviceIndex)ds.device);
+  auto cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)ds.device);
+  hipEvent_t pre = ds.get_event();
+  PDCC_HIP(hipEventRecord(pre, cur.stream()));
+  PDCC_HIP(hipStreamWaitEvent(ds.stream.stream(), pre, 0));
+  ds.put_event(pre);
+  const bool rx = cfg_.roctx && roctx_push_;
+  if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
+  {
+    c10::hip::HIPStreamGuard sg(ds.stream);  // temporaries + copy-backs run on the comm stream
+    fn(ds.stream.stream());
+  }
+  if (rx && roctx_pop_) roctx_pop_();
+  for (const auto& t : keep_alive)
+    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), ds.stream);
+  for (const auto& t : outputs)
+    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), ds.stream);
+  hipEvent_t ev;
+  PDCC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  PDCC_HIP(hipEventRecord(ev, ds.stream.stream()));
+  auto w = c10::make_intrusive<WorkMI355X>(rank_, [c] {
+    switch (c) {
+      case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
+      case Coll::REDUCE: return c10d::OpType::REDUCE;
+      case Coll::BROADCAST: return c10d::OpType::BROADCAST;
+      case Coll::ALLGATHER: return c10d::OpType::ALLGATHER;
+      case Coll::GATHER: return c10d::OpType::GATHER;
+      case Coll::SCATTER: return c10d::OpType::SCATTER;
+      case Coll::REDUCE_SCATTER: return c10d::OpType::REDUCE_SCATTER;
+      case Coll::ALLTOALL: return c10d::OpType::ALLTOALL;
+      case Coll::SEND: return c10d::OpType::SEND;
+      case Coll::RECV: return c10d::OpType::RECV;
+      default: return c10d::OpType::BARRIER;
+    }
+  }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, ds.stream,
+                                           health_, cfg_.blocking_wait, timeout, std::move(ipcp));
+  if (cfg_.watchdog_ms > 0) {
+    std::lock_guard<std::mutex> lk(wd_mu_);
+    inflight_.emplace_back(w);
+  }
+  return w;
+}
+
+// =================================================================== all-reduce / reduce
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, RedOpType op, int root, bool rooted,
+                                                                 std::chrono::milliseconds to) {
+  const Coll cname = rooted ? Coll::REDUCE : Coll::ALLREDUCE;
+  TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
+  DeviceState& ds = dev_state(t);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = t.nbytes();
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    record(cname, "local", bytes, t0);
+    return cpu_done(cname, {t});
+  }
+  kern::DType kd;
+  kern::RedOp ko;
+  const bool kok = kern_dtype(t.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
+  ncclDataType_t nd;
+  ncclRedOp_t no;
+  const bool nok = nccl_dtype(t.scalar_type(), nd) && nccl_op(op, t.scalar_type(), no);
+  const Algo a = choose(cname, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
+  if (a == Algo::HOST) {
+    at::Tensor h = t.cpu();
+    if (rooted) shm().reduce(h.data_ptr(), h.numel(), h.scalar_type(), op, root, to);
+    else shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
+    if (!rooted || rank_ == root) t.copy_(h);
+    record(cname, "host", bytes, t0);
+    return cpu_done(cname, {t});
+  }
+  at::Tensor w = prep_in(t);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  const bool one_shot = bytes <= cfg_.ipc_1shot_max;
+  auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = rooted ? (one_shot ? kern::IpcColl::REDUCE_1SHOT : kern::IpcColl::REDUCE_2SHOT)
+                      : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
+      c.dtype = kd;
+      c.op = ko;
+      c.root = root;
+      c.avg_div = size_;
+      c.bytes = bytes;
+      c.in[0] = w.data_ptr();
+      c.out[0] = w.data_ptr();
+      ipc_chunked(*icp, c, icp->max_staging(), s);
+    } else if (rooted) {
+      PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc->get(), s));
+    } else {
+      PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc->get(), s));
+    }
+    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+  }, icp);
+  record(cname, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  return work;
+}
+
+// =================================================================== broadcast
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, int root,
+                                                                 std::chrono::milliseconds to) {
+  DeviceState& ds = dev_state(t);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = t.nbytes();
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    record(Coll::BROADCAST, "local", bytes, t0);
+    return cpu_done(Coll::BROADCAST, {t});
+  }
+  const Algo a = choose(Coll::BROADCAST, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  if (a == Algo::HOST) {
+    at::Tensor h = t.cpu();
+    shm().broadcast(h.data_ptr(), h.nbytes(), root, to);
+    if (rank_ != root) t.copy_(h);
+    record(Coll::BROADCAST, "host", bytes, t0);
+    return cpu_done(Coll::BROADCAST, {t});
+  }
+  at::Tensor w = prep_in(t);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  const bool one_shot = bytes <= cfg_.ipc_1shot_max;
+  auto work = gpu_run(Coll::BROADCAST, ds, {t, w}, {t}, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = one_shot ? kern::IpcColl::BROADCAST_1SHOT : kern::IpcColl::BROADCAST_2SHOT;
+      c.dtype = kern::DType::U8;
+      c.op = kern::RedOp::COPY;
+      c.root = root;
+      c.bytes = bytes;
+      c.in[0] = w.data_ptr();
+      c.out[0] = w.data_ptr();
+      ipc_chunked(*icp, c, icp->max_staging(), s);
+    } else {
+      PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
+    }
+    if (!w.is_same(t) && rank_ != root) t.copy_(w);
+  }, icp);
+  record(Coll::BROADCAST, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  return work;
+}
+
+// =================================================================== all-gather / gather
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at::Tensor>& outs, at::Tensor& in,
+                                                                 int root, bool rooted,
+                                                                 std::chrono::milliseconds to) {
+  const Coll cname = rooted ? Coll::GATHER : Coll::ALLGATHER;
+  DeviceState& ds = dev_state(in);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = in.nbytes();
+  const bool receiver = !rooted || rank_ == root;
+  if (size_ == 1 && cfg_.world1_local) {
+    outs[0].copy_(in);
+    record(cname, "local", bytes, t0);
+    return cpu_done(cname, outs);
+  }
+  const Algo a = choose(cname, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  if (a == Algo::HOST) {
+    at::Tensor h = in.cpu();
+    std::vector<at::Tensor> ho;
+    std::vector<void*> ptrs(size_, nullptr);
+    if (receiver)
+      for (int r = 0; r < size_; ++r) {
+        ho.push_back(at::empty_like(h));
+        ptrs[r] = ho.back().data_ptr();
+      }
+    if (rooted) shm().gather(h.data_ptr(), ptrs, bytes, root, to);
+    else shm().allgather(h.data_ptr(), ptrs, bytes, to);
+    if (receiver)
+      for (int r = 0; r < size_; ++r) outs[r].copy_(ho[r]);
+    record(cname, "host", bytes, t0);
+    return cpu_done(cname, outs);
+  }
+  at::Tensor wi = prep_in(in);
+  std::vector<at::Tensor> wo;
+  if (receiver)
+    for (auto& o : outs) wo.push_back(prep_out(o));
+  std::vector<at::Tensor> keep{in, wi};
+  for (auto& o : wo) keep.push_back(o);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  const char* algo = a == Algo::IPC ? "ipc" : "rccl";
+  auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = rooted ? kern::IpcColl::GATHER : kern::IpcColl::ALLGATHER;
+      c.dtype = kern::DType::U8;
+      c.op = kern::RedOp::COPY;
+      c.root = root;
+      c.bytes = bytes;
+      c.in[0] = wi.data_ptr();
+      if (receiver)
+        for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
+      ipc_chunked(*icp, c, icp->max_staging(), s);
+    } else if (!rooted) {
+      if (is_flat(wo, bytes)) {
+        PDCC_NCCL(ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc->get(), s));
+      } else {
+        at::Tensor stg = at::empty({(int64_t)(bytes * size_)}, in.options().dtype(at::kByte));
+        PDCC_NCCL(ncclAllGather(wi.data_ptr(), stg.data_ptr(), bytes, ncclUint8, rc->get(), s));
+        std::vector<kern::CopyDesc> d;
+        for (int r = 0; r < size_; ++r) d.push_back({static_cast<char*>(stg.data_ptr()) + r * bytes, wo[r].data_ptr(), bytes});
+        multi_copy_or_memcpy(d, s);  // K2 unpack
+      }
+    } else {
+      PDCC_NCCL(ncclGroupStart());
+      if (rank_ == root) {
+        for (int r = 0; r < size_; ++r)
+          if (r != root) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), bytes, ncclUint8, r, rc->get(), s));
+      } else {
+        PDCC_NCCL(ncclSend(wi.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
+      }
+      PDCC_NCCL(ncclGroupEnd());
+      if (rank_ == root) PDCC_HIP(hipMemcpyAsync(wo[root].data_ptr(), wi.data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
+    }
+    if (receiver)
+      for (int r = 0; r < size_; ++r)
+        if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+  }, icp);
+  record(cname, algo, bytes, t0);
+  return work;
+}
+
+// =================================================================== scatter
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
+                                                               int root, std::chrono::milliseconds to) {
+  DeviceState& ds = dev_state(out);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = out.nbytes();
+  if (size_ == 1 && cfg_.world1_local) {
+    out.copy_(ins[0]);
+    record(Coll::SCATTER, "local", bytes, t0);
+    return cpu_done(Coll::SCATTER, {out});
+  }
+  const Algo a = choose(Coll::SCATTER, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  if (a == Algo::HOST) {
+    std::vector<at::Tensor> hi;
+    std::vector<const void*> ptrs(size_, nullptr);
+    if (rank_ == root)
+      for (int r = 0; r < size_; ++r) {
+        hi.push_back(ins[r].cpu().contiguous());
+        ptrs[r] = hi.back().data_ptr();
+      }
+    at::Tensor h = at::empty(out.sizes(), out.options().device(at::kCPU));
+    shm().scatter(ptrs, h.data_ptr(), bytes, root, to);
+    out.copy_(h);
+    record(Coll::SCATTER, "host", bytes, t0);
+    return cpu_done(Coll::SCATTER, {out});
+  }
+  std::vector<at::Tensor> wi;
+  if (rank_ == root)
+    for (auto& i : ins) wi.push_back(prep_in(i));
+  at::Tensor wo = prep_out(out);
+  std::vector<at::Tensor> keep{out, wo};
+  for (auto& i : wi) keep.push_back(i);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  auto work = gpu_run(Coll::SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = kern::IpcColl::SCATTER;
+      c.dtype = kern::DType::U8;
+      c.op = kern::RedOp::COPY;
+      c.root = root;
+      c.bytes = bytes;
+      if (rank_ == root)
+        for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
+      c.out[0] = wo.data_ptr();
+      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
+    } else {
+      PDCC_NCCL(ncclGroupStart());
+      if (rank_ == root) {
+        for (int r = 0; r < size_; ++r)
+          if (r != root) PDCC_NCCL(ncclSend(wi[r].data_ptr(), bytes, ncclUint8, r, rc->get(), s));
+      } else {
+        PDCC_NCCL(ncclRecv(wo.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
+      }
+      PDCC_NCCL(ncclGroupEnd());
+      if (rank_ == root) PDCC_HIP(hipMemcpyAsync(wo.data_ptr(), wi[root].data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
+    }
+    if (!wo.is_same(out)) out.copy_(wo);
+  }, icp);
+  record(Coll::SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
+  return work;
+}
+
+// =================================================================== reduce-scatter
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
+                                                                      RedOpType op, std::chrono::milliseconds to) {
+  TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
+  DeviceState& ds = dev_state(out);
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = out.nbytes();
+  if (size_ == 1 && cfg_.world1_local) {
+    out.copy_(ins[0]);
+    record(Coll::REDUCE_SCATTER, "local", bytes, t0);
+    return cpu_done(Coll::REDUCE_SCATTER, {out});
+  }
+  kern::DType kd;
+  kern::RedOp ko;
+  const bool kok = kern_dtype(out.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
+  ncclDataType_t nd;
+  ncclRedOp_t no;
+  const bool nok = nccl_dtype(out.scalar_type(), nd) && nccl_op(op, out.scalar_type(), no);
+  const Algo a = choose(Coll::REDUCE_SCATTER, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
+  if (a == Algo::HOST) {
+    std::vector<at::Tensor> hi;
+    std::vector<const void*> ptrs;
+    for (auto& i : ins) {
+      hi.push_back(i.cpu().contiguous());
+      ptrs.push_back(hi.back().data_ptr());
+    }
+    at::Tensor h = at::empty(out.sizes(), out.options().device(at::kCPU));
+    shm().reduce_scatter(ptrs, h.data_ptr(), out.numel(), out.scalar_type(), op, to);
+    out.copy_(h);
+    record(Coll::REDUCE_SCATTER, "host", bytes, t0);
+    return cpu_done(Coll::REDUCE_SCATTER, {out});
+  }
+  std::vector<at::Tensor> wi;
+  for (auto& i : ins) wi.push_back(prep_in(i));
+  at::Tensor wo = prep_out(out);
+  std::vector<at::Tensor> keep{out, wo};
+  for (auto& i : wi) keep.push_back(i);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  auto work = gpu_run(Coll::REDUCE_SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = kern::IpcColl::REDUCE_SCATTER;
+      c.dtype = kd;
+      c.op = ko;
+      c.avg_div = size_;
+      c.bytes = bytes;
+      for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
+      c.out[0] = wo.data_ptr();
+      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
+    } else {
+      const void* src;
+      at::Tensor stg;
+      if (is_flat(wi, bytes)) {
+        src = wi[0].data_ptr();
+      } else {  // K2 pack into one staging buffer
+        stg = at::empty({(int64_t)(bytes * size_)}, out.options().dtype(at::kByte));
+        std::vector<kern::CopyDesc> d;
+        for (int r = 0; r < size_; ++r) d.push_back({wi[r].data_ptr(), static_cast<char*>(stg.data_ptr()) + r * bytes, bytes});
+        multi_copy_or_memcpy(d, s);
+        src = stg.data_ptr();
+      }
+      PDCC_NCCL(ncclReduceScatter(src, wo.data_ptr(), out.numel(), nd, no, rc->get(), s));
+    }
+    if (!wo.is_same(out)) out.copy_(wo);
+  }, icp);
+  record(Coll::REDUCE_SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
+  return work;
+}
+
+// =================================================================== all-to-all
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::Tensor>& outs,
+                                                                std::vector<at::Tensor>& ins, bool equal,
+                                                                std::chrono::milliseconds to) {
+  DeviceState& ds = dev_state(ins[0]);
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t total = 0;
+  for (auto& i : ins) total += i.nbytes();
+  if (size_ == 1 && cfg_.world1_local) {
+    outs[0].copy_(ins[0]);
+    record(Coll::ALLTOALL, "local", total, t0);
+    return cpu_done(Coll::ALLTOALL, outs);
+  }
+  const size_t chunk = ins[0].nbytes();
+  const Algo a = choose(Coll::ALLTOALL, equal ? chunk : SIZE_MAX, ds, ds.rccl_ok, ds.ipc_ok && equal);
+  if (a == Algo::HOST) {
+    std::vector<at::Tensor> hi, ho;
+    std::vector<const void*> ip;
+    std::vector<void*> op;
+    std::vector<size_t> sb, rb;
+    for (auto& i : ins) {
+      hi.push_back(i.cpu().contiguous());
+      ip.push_back(hi.back().data_ptr());
+      sb.push_back(hi.back().nbytes());
+    }
+    for (auto& o : outs) {
+      ho.push_back(at::empty(o.sizes(), o.options().device(at::kCPU)));
+      op.push_back(ho.back().data_ptr());
+      rb.push_back(ho.back().nbytes());
+    }
+    shm().alltoall(ip, sb, op, rb, to);
+    for (size_t i = 0; i < outs.size(); ++i) outs[i].copy_(ho[i]);
+    record(Coll::ALLTOALL, "host", total, t0);
+    return cpu_done(Coll::ALLTOALL, outs);
+  }
+  std::vector<at::Tensor> wi, wo, keep;
+  for (auto& i : ins) wi.push_back(prep_in(i));
+  for (auto& o : outs) wo.push_back(prep_out(o));
+  for (auto& x : wi) keep.push_back(x);
+  for (auto& x : wo) keep.push_back(x);
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
+  auto work = gpu_run(Coll::ALLTOALL, ds, keep, outs, to, [&](hipStream_t s) {
+    if (a == Algo::IPC) {
+      kern::IpcCall c{};
+      c.coll = kern::IpcColl::ALLTOALL;
+      c.dtype = kern::DType::U8;
+      c.op = kern::RedOp::COPY;
+      c.bytes = chunk;
+      for (int r = 0; r < size_; ++r) {
+        c.in[r] = wi[r].data_ptr();
+        c.out[r] = wo[r].data_ptr();
+      }
+      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
+    } else if (equal && is_flat(wi, chunk) && is_flat(wo, chunk)) {
+      PDCC_NCCL(ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc->get(), s));
+    } else {
+      PDCC_NCCL(ncclGroupStart());
+      for (int r = 0; r < size_; ++r) {
+        if (r == rank_) continue;
+        if (wi[r].nbytes()) PDCC_NCCL(ncclSend(wi[r].data_ptr(), wi[r].nbytes(), ncclUint8, r, rc->get(), s));
+        if (wo[r].nbytes()) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), wo[r].nbytes(), ncclUint8, r, rc->get(), s));
+      }
+      PDCC_NCCL(ncclGroupEnd());
+      if (wi[rank_].nbytes())
+        PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi[rank_].data_ptr(), wi[rank_].nbytes(),
+                                hipMemcpyDeviceToDevice, s));
+    }
+    for (size_t i = 0; i < outs.size(); ++i)
+      if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
+  }, icp);
+  record(Coll::ALLTOALL, a == Algo::IPC ? "ipc" : "rccl", total, t0);
+  return work;
+}
+
+// =================================================================== p2p + coalescing
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int peer, bool is_send,
+                                                           std::chrono::milliseconds to) {
+  DeviceState& ds = dev_state(t);
+  const auto t0 = std::chrono::steady_clock::now();
+  const Coll cname = is_send ? Coll::SEND : Coll::RECV;
+  if (!ds.rccl_ok || cfg_.force_algo == Algo::HOST) {
+    // shared-device setups: through the host transport, synchronously
+    if (is_send) {
+      at::Tensor h = t.cpu().contiguous();
+      shm().send(h.data_ptr(), h.nbytes(), peer, to);
+    } else {
+      at::Tensor h = at::empty(t.sizes(), t.options().device(at::kCPU));
+      shm().recv(h.data_ptr(), h.nbytes(), peer, to);
+      t.copy_(h);
+    }
+    record(cname, "host", t.nbytes(), t0);
+    return cpu_done(cname, {t});
+  }
+  RcclComm& rc = rccl(ds);
+  at::Tensor w = is_send ? prep_in(t) : prep_out(t);
+  auto op = [w, t, peer, is_send, comm = rc.get()](hipStream_t s) mutable {
+    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
+    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
+  };
+  if (coalescing_) {
+    coalesced_.push_back(op);
+    coalesced_tensors_.push_back(t);
+    coalesced_tensors_.push_back(w);
+    coalesced_ds_ = &ds;
+    record(cname, "rccl_coalesced", t.nbytes(), t0);
+    return cpu_done(cname, {t});
+  }
+  auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
+    op(s);
+    if (!is_send && !w.is_same(t)) t.copy_(w);
+  });
+  record(cname, "rccl", t.nbytes(), t0);
+  return work;
+}
+
+void ProcessGroupMI355X::startCoalescing() {
+  coalescing_ = true;
+  coalesced_cpu_.clear();
+  coalesced_.clear();
+  coalesced_tensors_.clear();
+  coalesced_ds_ = nullptr;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::endCoalescing() {
+  coalescing_ = false;
+  DeviceState* ds = coalesced_ds_;
+  if (!ds) {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    if (devs_.size() == 1) ds = devs_.begin()->second.get();
+  }
+  // CPU p2p posted inside the batch runs on the worker threads: wait for all of
+  // it so the returned work really covers the batch (all ops are already posted,
+  // so this cannot deadlock the exchange)
+  auto cpu_works = std::move(coalesced_cpu_);
+  coalesced_cpu_.clear();
+  for (auto& w : cpu_works) w->wait();
+  if (!ds) return cpu_done(Coll::SEND, {});
+  auto fns = std::move(coalesced_);
+  auto keep = std::move(coalesced_tensors_);
+  coalesced_.clear();
+  coalesced_tensors_.clear();
+  coalesced_ds_ = nullptr;
+  return gpu_run(Coll::SEND, *ds, keep, {}, timeout_, [&](hipStream_t s) {
+    if (fns.empty()) return;
+    PDCC_NCCL(ncclGroupStart());
+    for (auto& f : fns) f(s);
+    PDCC_NCCL(ncclGroupEnd());
+    for (size_t i = 0; i + 1 < keep.size(); i += 2)
+      if (!keep[i].is_same(keep[i + 1])) keep[i].copy_(keep[i + 1]);
+  });
+}
+
+}  // namespace pdcc

@@ -1,0 +1,878 @@
+// ProcessGroupMI355X: construction, Work objects, CPU (shared-memory) paths,
+// argument validation, debug fingerprinting, fault injection and the watchdog.
+// GPU data paths live in gpu_ops.cpp.
+#include "process_group.h"
+
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+#include "../device/comm_util.h"
+
+namespace pdcc {
+
+// =================================================================== Work
+WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs,
+                       std::exception_ptr err)
+    : c10d::Work(rank, type), seq_(seq), outputs_(std::move(outputs)), start_(std::chrono::steady_clock::now()) {
+  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()));
+  if (err) {
+    fut_->setError(err);
+    finish(err);
+  } else {
+    fut_->markCompleted(c10::IValue(outputs_));
+    finish();
+  }
+}
+
+WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs)
+    : c10d::Work(rank, type), seq_(seq), outputs_(std::move(outputs)), start_(std::chrono::steady_clock::now()) {
+  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()));
+}
+
+WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs, c10::Device dev,
+                       hipEvent_t ev, c10::hip::HIPStream comm, std::shared_ptr<Health> health, bool blocking,
+                       std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc)
+    : c10d::Work(rank, type),
+      seq_(seq),
+      gpu_(true),
+      outputs_(std::move(outputs)),
+      dev_(dev),
+      ev_(ev),
+      health_(std::move(health)),
+      ipc_(std::move(ipc)),
+      blocking_(blocking),
+      timeout_(timeout),
+      start_(std::chrono::steady_clock::now()) {
+  std::vector<c10::Device> devs{dev_};
+  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
+  c10::hip::HIPStreamGuard g(comm);  // the future's events are recorded on the comm stream
+  fut_->markCompleted(c10::IValue(outputs_));
+}
+
+WorkMI355X::~WorkMI355X() {
+  if (ev_) hipEventDestroy(ev_);
+}
+
+void WorkMI355X::done(std::exception_ptr e) {
+  if (e) fut_->setError(e);
+  else fut_->markCompleted(c10::IValue(outputs_));
+  finish(e);
+}
+
+void WorkMI355X::fail(const std::string& msg) {
+  std::lock_guard<std::mutex> lk(mutex_);
+  if (!exception_) exception_ = std::make_exception_ptr(std::runtime_error(msg));
+}
+
+bool WorkMI355X::gpu_event_done() {
+  if (!ev_) return true;
+  return hipEventQuery(ev_) == hipSuccess;
+}
+
+void WorkMI355X::check_health() {
+  if (health_ && health_->poisoned.load())
+    throw std::runtime_error("pdcc: process group is in an error state: " + health_->message());
+  if (ipc_ && ipc_->error_word() != 0)
+    throw std::runtime_error("pdcc: an IPC collective timed out waiting for a peer (error word " +
+                             std::to_string(ipc_->error_word()) + ")");
+  std::lock_guard<std::mutex> lk(mutex_);
+  if (exception_) std::rethrow_exception(exception_);
+}
+
+bool WorkMI355X::isCompleted() {
+  if (!gpu_) return c10d::Work::isCompleted();
+  if (health_ && health_->poisoned.load()) return true;
+  return gpu_event_done();
+}
+
+bool WorkMI355X::isSuccess() const {
+  if (!gpu_) return c10d::Work::isSuccess();
+  if (health_ && health_->poisoned.load()) return false;
+  std::lock_guard<std::mutex> lk(mutex_);
+  return !exception_;
+}
+
+void WorkMI355X::synchronize() {
+  if (!gpu_) return;
+  c10::hip::HIPGuard g(dev_);
+  auto cur = c10::hip::getCurrentHIPStream(dev_.index());
+  PDCC_HIP(hipStreamWaitEvent(cur.stream(), ev_, 0));
+}
+
+bool WorkMI355X::wait(std::chrono::milliseconds timeout) {
+  if (!gpu_) return c10d::Work::wait(timeout);
+  check_health();
+  synchronize();  // current stream waits for the collective: host not blocked
+  if (blocking_ || timeout != kNoTimeout) {
+    const auto lim = (timeout == kNoTimeout) ? timeout_ : timeout;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!gpu_event_done()) {
+      check_health();
+      if (std::chrono::steady_clock::now() - t0 > lim)
+        throw std::runtime_error("pdcc: Work.wait() timed out after " + std::to_string(lim.count()) + " ms");
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    check_health();
+  }
+  return true;
+}
+
+std::vector<at::Tensor> WorkMI355X::result() { return outputs_; }
+c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() { return fut_; }
+
+// =================================================================== DeviceState
+hipEvent_t DeviceState::get_event() {
+  std::lock_guard<std::mutex> lk(ev_mu);
+  if (!ev_pool.empty()) {
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  PDCC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return e;
+}
+void DeviceState::put_event(hipEvent_t e) {
+  std::lock_guard<std::mutex> lk(ev_mu);
+  ev_pool.push_back(e);
+}
+
+// =================================================================== helpers
+namespace {
+
+c10d::OpType op_type_of(int c) {
+  switch (c) {
+    case 0: return c10d::OpType::ALLREDUCE;
+    case 1: return c10d::OpType::REDUCE;
+    case 2: return c10d::OpType::BROADCAST;
+    case 3: return c10d::OpType::ALLGATHER;
+    case 4: return c10d::OpType::GATHER;
+    case 5: return c10d::OpType::SCATTER;
+    case 6: return c10d::OpType::REDUCE_SCATTER;
+    case 7: return c10d::OpType::ALLTOALL;
+    case 8: return c10d::OpType::SEND;
+    case 9: return c10d::OpType::RECV;
+    default: return c10d::OpType::BARRIER;
+  }
+}
+
+std::string shape_str(const at::Tensor& t) {
+  std::ostringstream o;
+  o << c10::toString(t.scalar_type()) << "[" << t.numel() << "]@" << t.device();
+  return o.str();
+}
+
+void check_single(const std::vector<at::Tensor>& ts, const char* fn) {
+  TORCH_CHECK(ts.size() == 1, "ProcessGroupMI355X::", fn, ": expects exactly one tensor per call, got ", ts.size());
+}
+
+void check_root(int64_t root, int size, const char* fn) {
+  TORCH_CHECK(root >= 0 && root < size, "ProcessGroupMI355X::", fn, ": invalid root rank: ", root);
+}
+
+void check_list(const std::vector<at::Tensor>& list, const at::Tensor& like, int size, const char* fn,
+                const char* what) {
+  TORCH_CHECK((int)list.size() == size, "ProcessGroupMI355X::", fn, ": invalid ", what,
+              " tensor list at index 0 (expected length ", size, ", got ", list.size(), ")");
+  for (size_t i = 0; i < list.size(); ++i) {
+    TORCH_CHECK(list[i].scalar_type() == like.scalar_type(), "ProcessGroupMI355X::", fn, ": ", what,
+                " tensor ", i, " has dtype ", list[i].scalar_type(), ", expected ", like.scalar_type());
+    TORCH_CHECK(list[i].numel() == like.numel(), "ProcessGroupMI355X::", fn, ": ", what, " tensor ", i, " has ",
+                list[i].numel(), " elements, expected ", like.numel());
+    TORCH_CHECK(list[i].device() == like.device(), "ProcessGroupMI355X::", fn, ": ", what, " tensor ", i,
+                " is on ", list[i].device(), ", expected ", like.device());
+  }
+}
+
+void check_cpu_dtype(at::ScalarType t, c10d::ReduceOp::RedOpType op, const char* fn) {
+  const bool fl = at::isFloatingType(t);
+  const bool integral = at::isIntegralType(t, /*includeBool=*/true);
+  TORCH_CHECK(fl || integral, "ProcessGroupMI355X::", fn, ": unsupported dtype ", t);
+  TORCH_CHECK(op != c10d::ReduceOp::PREMUL_SUM, "ProcessGroupMI355X::", fn, ": PREMUL_SUM is not supported");
+  if (op == c10d::ReduceOp::BAND || op == c10d::ReduceOp::BOR || op == c10d::ReduceOp::BXOR)
+    TORCH_CHECK(!fl, "ProcessGroupMI355X::", fn, ": bitwise reductions need an integer dtype, got ", t);
+  if (op == c10d::ReduceOp::AVG) TORCH_CHECK(t != at::kBool, "ProcessGroupMI355X::", fn, ": AVG on bool");
+}
+
+// contiguous host staging copy (CPU tensors may be strided views)
+struct Contig {
+  at::Tensor orig, work;
+  explicit Contig(const at::Tensor& t) : orig(t), work(t.is_contiguous() ? t : t.contiguous()) {}
+  void* ptr() { return work.data_ptr(); }
+  void write_back() {
+    if (!work.is_same(orig)) orig.copy_(work);
+  }
+};
+
+}  // namespace
+
+const char* ProcessGroupMI355X::coll_name(Coll c) {
+  switch (c) {
+    case Coll::ALLREDUCE: return "allreduce";
+    case Coll::REDUCE: return "reduce";
+    case Coll::BROADCAST: return "broadcast";
+    case Coll::ALLGATHER: return "allgather";
+    case Coll::GATHER: return "gather";
+    case Coll::SCATTER: return "scatter";
+    case Coll::REDUCE_SCATTER: return "reduce_scatter";
+    case Coll::ALLTOALL: return "alltoall";
+    case Coll::SEND: return "send";
+    case Coll::RECV: return "recv";
+    case Coll::BARRIER: return "barrier";
+  }
+  return "?";
+}
+
+// roctx ranges (optional, resolved with dlopen so there is no link dependency)
+namespace {
+struct Roctx {
+  int (*push)(const char*) = nullptr;
+  int (*pop)() = nullptr;
+  Roctx() {
+    for (const char* lib : {"librocprofiler-sdk-roctx.so", "libroctx64.so"}) {
+      void* h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+      if (!h) continue;
+      push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+      pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+      if (push && pop) break;
+    }
+  }
+};
+Roctx& roctx() {
+  static Roctx r;
+  return r;
+}
+}  // namespace
+
+// =================================================================== construction
+ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
+                                       std::chrono::milliseconds timeout, std::vector<int64_t> global_ranks,
+                                       std::string group_name)
+    : c10d::Backend(rank, size),
+      store_(store),
+      timeout_(timeout),
+      global_ranks_(std::move(global_ranks)),
+      group_name_(std::move(group_name)),
+      cfg_(Config::from_env()),
+      health_(std::make_shared<Health>()) {
+  if (!cfg_.fault.empty()) {
+    unsigned long long s = 0;
+    char kind[32] = {0};
+    int r = -1;
+    if (sscanf(cfg_.fault.c_str(), "%d:%llu:%31s", &r, &s, kind) == 3) {
+      fault_rank_ = r;
+      fault_seq_ = s;
+      fault_kind_ = kind;
+    }
+  }
+  // topology: all ranks of this group on one host? (shm host path + IPC need it)
+  char host[256] = {0};
+  gethostname(host, sizeof(host) - 1);
+  const std::string h(host);
+  const auto all = store_allgather(store_, "pdcc/topo", rank, size, std::vector<uint8_t>(h.begin(), h.end()));
+  for (const auto& v : all) same_host_ = same_host_ && (std::string(v.begin(), v.end()) == h);
+  if (cfg_.log_level >= 1 && rank == 0)
+    fprintf(stderr, "[pdcc] group '%s' size=%d same_host=%d %s\n", group_name_.c_str(), size, (int)same_host_,
+            cfg_.describe().c_str());
+  if (cfg_.roctx) {
+    roctx_push_ = roctx().push;
+    roctx_pop_ = roctx().pop;
+  }
+  if (cfg_.watchdog_ms > 0) wd_thr_ = std::thread([this] { watchdog_loop(); });
+}
+
+ProcessGroupMI355X::~ProcessGroupMI355X() {
+  wd_stop_.store(true);
+  if (wd_thr_.joinable()) wd_thr_.join();
+  {
+    std::lock_guard<std::mutex> lk(p2p_mu_);
+    stop_ = true;
+  }
+  p2p_cv_.notify_all();
+  if (send_thr_.joinable()) send_thr_.join();
+  if (recv_thr_.joinable()) recv_thr_.join();
+  for (auto& kv : devs_) {
+    DeviceState& ds = *kv.second;
+    if (health_->poisoned.load() && ds.rccl) ds.rccl->abort();
+    for (hipEvent_t e : ds.ev_pool) hipEventDestroy(e);
+  }
+}
+
+std::chrono::milliseconds ProcessGroupMI355X::eff_timeout(std::chrono::milliseconds t) const {
+  return t == c10d::kUnsetTimeout ? timeout_ : t;
+}
+
+host::ShmComm& ProcessGroupMI355X::shm() {
+  std::lock_guard<std::mutex> lk(init_mu_);
+  if (!shm_) {
+    TORCH_CHECK(same_host_, "pdcc: the shared-memory host path needs every rank of the group on one host");
+    host::ShmConfig sc;
+    sc.slot_bytes = cfg_.shm_slot_bytes;
+    sc.chan_bytes = size_ > 16 ? std::min<size_t>(cfg_.shm_chan_bytes, 256u << 10) : cfg_.shm_chan_bytes;
+    sc.timeout = timeout_;
+    shm_ = std::make_unique<host::ShmComm>(store_, "pdcc/shm", rank_, size_, sc);
+  }
+  return *shm_;
+}
+
+void ProcessGroupMI355X::maybe_inject_fault() {
+  const uint64_t s = op_seq_.load();
+  if (fault_rank_ != rank_ || fault_seq_ != s) return;
+  fprintf(stderr, "[pdcc] rank %d: injecting fault '%s' at op %llu\n", rank_, fault_kind_.c_str(),
+          (unsigned long long)s);
+  fflush(stderr);
+  if (fault_kind_ == "exit") _exit(13);
+  if (fault_kind_ == "hang")
+    for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+  throw std::runtime_error("pdcc: injected fault at op " + std::to_string(s));
+}
+
+void ProcessGroupMI355X::before_op(Coll c, const std::vector<at::Tensor>& ts, int root) {
+  if (health_->poisoned.load())
+    throw std::runtime_error("pdcc: process group is in an error state: " + health_->message());
+  ++op_seq_;
+  maybe_inject_fault();
+  if (cfg_.debug && c != Coll::SEND && c != Coll::RECV) debug_check(c, ts, root);
+  if (cfg_.log_level >= 2)
+    fprintf(stderr, "[pdcc r%d] #%llu %s %s root=%d\n", rank_, (unsigned long long)op_seq_.load(), coll_name(c),
+            ts.empty() ? "-" : shape_str(ts[0]).c_str(), root);
+}
+
+// PDCC_DEBUG=1: every rank publishes a fingerprint of the op it is about to run
+// and compares it with everyone else's -- catches the silent desync the survey
+// found with Gloo (per-rank shape mismatch: rank 0 "OK", rank 1 error).
+void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, int root) {
+  struct Fp {
+    uint64_t seq;
+    int32_t coll, dtype;
+    int64_t numel;
+    int32_t root, dev_type;
+  };
+  Fp mine{op_seq_.load(), (int32_t)c, ts.empty() ? -1 : (int32_t)ts[0].scalar_type(),
+          ts.empty() ? 0 : ts[0].numel(), root, ts.empty() ? -1 : (int32_t)ts[0].device().type()};
+  std::vector<Fp> all(size_);
+  std::vector<void*> outs(size_);
+  for (int r = 0; r < size_; ++r) outs[r] = &all[r];
+  shm().allgather(&mine, outs, sizeof(Fp), timeout_);
+  for (int r = 0; r < size_; ++r) {
+    const Fp& f = all[r];
+    if (f.seq != mine.seq || f.coll != mine.coll || f.dtype != mine.dtype || f.numel != mine.numel ||
+        f.root != mine.root || f.dev_type != mine.dev_type) {
+      std::ostringstream o;
+      o << "pdcc DEBUG: collective mismatch at op #" << mine.seq << ": rank " << rank_ << " runs "
+        << coll_name(c) << "(dtype=" << mine.dtype << ", numel=" << mine.numel << ", root=" << mine.root
+        << ") but rank " << r << " runs " << coll_name((Coll)f.coll) << "(dtype=" << f.dtype
+        << ", numel=" << f.numel << ", root=" << f.root << ", op #" << f.seq << ")";
+      throw std::runtime_error(o.str());
+    }
+  }
+}
+
+void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0) {
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  OpStats& s = stats_[std::string(coll_name(c)) + "/" + algo];
+  s.calls++;
+  s.bytes += bytes;
+  s.host_ms += ms;
+  last_algo_ = algo;
+}
+
+std::map<std::string, OpStats> ProcessGroupMI355X::stats() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  return stats_;
+}
+void ProcessGroupMI355X::reset_stats() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  stats_.clear();
+}
+
+std::string ProcessGroupMI355X::describe() {
+  std::ostringstream o;
+  o << "ProcessGroupMI355X(group=" << group_name_ << ", rank=" << rank_ << ", size=" << size_
+    << ", same_host=" << same_host_ << ", timeout_ms=" << timeout_.count() << ", " << cfg_.describe();
+  std::lock_guard<std::mutex> lk(init_mu_);
+  for (auto& kv : devs_)
+    o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
+      << ", shared_device=" << kv.second->shared_device << ", rccl=" << (kv.second->rccl != nullptr)
+      << ", ipc=" << (kv.second->ipc != nullptr) << "}";
+  o << ")";
+  return o.str();
+}
+
+void ProcessGroupMI355X::abort_group(const std::string& why) {
+  health_->poison(why);
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    for (auto& kv : devs_)
+      if (kv.second->rccl) kv.second->rccl->abort();
+    if (shm_) shm_->abort();
+  }
+}
+
+void ProcessGroupMI355X::set_algo(const std::string& a) {
+  if (a == "auto") cfg_.force_algo = Algo::AUTO;
+  else if (a == "rccl") cfg_.force_algo = Algo::RCCL;
+  else if (a == "ipc") cfg_.force_algo = Algo::IPC;
+  else if (a == "host") cfg_.force_algo = Algo::HOST;
+  else TORCH_CHECK(false, "set_algo: expected auto|rccl|ipc|host, got ", a);
+}
+
+void ProcessGroupMI355X::set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max) {
+  if (one_shot_max >= 0) cfg_.ipc_1shot_max = (size_t)one_shot_max;
+  if (two_shot_max >= 0) cfg_.ipc_2shot_max = (size_t)two_shot_max;
+  if (copy_max >= 0) cfg_.ipc_copy_max = (size_t)copy_max;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::cpu_done(Coll c, std::vector<at::Tensor> outputs) {
+  return c10::make_intrusive<WorkMI355X>(rank_, op_type_of((int)c), op_seq_.load(), std::move(outputs), nullptr);
+}
+
+// =================================================================== watchdog
+void ProcessGroupMI355X::watchdog_loop() {
+  while (!wd_stop_.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.watchdog_ms));
+    std::vector<c10::intrusive_ptr<WorkMI355X>> live;
+    {
+      std::lock_guard<std::mutex> lk(wd_mu_);
+      std::vector<c10::weak_intrusive_ptr<WorkMI355X>> keep;
+      for (auto& w : inflight_) {
+        auto s = w.lock();
+        if (!s) continue;
+        live.push_back(s);
+      }
+      inflight_.clear();
+      for (auto& s : live) inflight_.emplace_back(s);
+    }
+    std::vector<c10::intrusive_ptr<WorkMI355X>> still;
+    const auto now = std::chrono::steady_clock::now();
+    for (auto& w : live) {
+      if (w->gpu_event_done()) continue;
+      if (now - w->start() > w->timeout()) {
+        const std::string msg = "watchdog: collective #" + std::to_string(w->getSequencenumber()) + " on rank " +
+                                std::to_string(rank_) + " exceeded its timeout of " +
+                                std::to_string(w->timeout().count()) + " ms; aborting the group";
+        fprintf(stderr, "[pdcc] %s\n", msg.c_str());
+        w->fail(msg);
+        abort_group(msg);
+        continue;
+      }
+      still.push_back(w);
+    }
+    {
+      std::lock_guard<std::mutex> lk(wd_mu_);
+      std::vector<c10::weak_intrusive_ptr<WorkMI355X>> merged;
+      for (auto& w : inflight_) {
+        auto s = w.lock();
+        if (s && !s->gpu_event_done()) merged.emplace_back(s);
+      }
+      inflight_.swap(merged);
+    }
+    // asynchronous RCCL errors and IPC spin timeouts poison the group
+    std::lock_guard<std::mutex> lk(init_mu_);
+    for (auto& kv : devs_) {
+      DeviceState& ds = *kv.second;
+      if (ds.rccl) {
+        ncclResult_t r = ds.rccl->async_error();
+        if (r != ncclSuccess && r != ncclInProgress) {
+          const std::string m = std::string("RCCL async error: ") + ncclGetErrorString(r);
+          fprintf(stderr, "[pdcc] rank %d: %s\n", rank_, m.c_str());
+          health_->poison(m);
+          ds.rccl->abort();
+        }
+      }
+      if (ds.ipc && ds.ipc->error_word() != 0 && !health_->poisoned.load()) {
+        const std::string m = "IPC collective timed out waiting for a peer (error word " +
+                              std::to_string(ds.ipc->error_word()) + ")";
+        fprintf(stderr, "[pdcc] rank %d: %s\n", rank_, m.c_str());
+        health_->poison(m);
+      }
+    }
+  }
+}
+
+// =================================================================== p2p threads (CPU)
+void ProcessGroupMI355X::p2p_loop(std::deque<Job>* q, bool* stop) {
+  for (;;) {
+    Job j;
+    {
+      std::unique_lock<std::mutex> lk(p2p_mu_);
+      p2p_cv_.wait(lk, [&] { return *stop || !q->empty(); });
+      if (q->empty()) return;
+      j = std::move(q->front());
+      q->pop_front();
+    }
+    std::exception_ptr e;
+    try {
+      j.fn();
+    } catch (...) {
+      e = std::current_exception();
+    }
+    j.work->done(e);
+  }
+}
+
+void ProcessGroupMI355X::p2p_submit(bool is_send, Job j) {
+  std::lock_guard<std::mutex> lk(p2p_mu_);
+  if (is_send && !send_thr_.joinable()) send_thr_ = std::thread([this] { p2p_loop(&send_q_, &stop_); });
+  if (!is_send && !recv_thr_.joinable()) recv_thr_ = std::thread([this] { p2p_loop(&recv_q_, &stop_); });
+  (is_send ? send_q_ : recv_q_).push_back(std::move(j));
+  p2p_cv_.notify_all();
+}
+
+// =================================================================== collectives
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce(std::vector<at::Tensor>& tensors,
+                                                             const c10d::AllreduceOptions& opts) {
+  check_single(tensors, "allreduce");
+  at::Tensor& t = tensors[0];
+  before_op(Coll::ALLREDUCE, tensors, -1);
+  if (t.is_cuda()) return gpu_allreduce(t, opts.reduceOp.op_, -1, false, eff_timeout(opts.timeout));
+  check_cpu_dtype(t.scalar_type(), opts.reduceOp.op_, "allreduce");
+  const auto t0 = std::chrono::steady_clock::now();
+  if (size_ > 1) {
+    Contig c(t);
+    shm().allreduce(c.ptr(), t.numel(), t.scalar_type(), opts.reduceOp.op_, eff_timeout(opts.timeout));
+    c.write_back();
+  }
+  record(Coll::ALLREDUCE, "shm", t.nbytes(), t0);
+  return cpu_done(Coll::ALLREDUCE, tensors);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce_coalesced(std::vector<at::Tensor>& tensors,
+                                                                       const c10d::AllreduceCoalescedOptions& opts) {
+  c10::intrusive_ptr<c10d::Work> last;
+  for (auto& t : tensors) {
+    std::vector<at::Tensor> one{t};
+    c10d::AllreduceOptions o;
+    o.reduceOp = opts.reduceOp;
+    o.timeout = opts.timeout;
+    last = allreduce(one, o);
+  }
+  if (!last) return cpu_done(Coll::ALLREDUCE, {});
+  // all pieces ran on the same stream: waiting on the last one orders them all
+  return last;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce(std::vector<at::Tensor>& tensors,
+                                                          const c10d::ReduceOptions& opts) {
+  check_single(tensors, "reduce");
+  check_root(opts.rootRank, size_, "reduce");
+  at::Tensor& t = tensors[0];
+  before_op(Coll::REDUCE, tensors, (int)opts.rootRank);
+  if (t.is_cuda()) return gpu_allreduce(t, opts.reduceOp.op_, (int)opts.rootRank, true, eff_timeout(opts.timeout));
+  check_cpu_dtype(t.scalar_type(), opts.reduceOp.op_, "reduce");
+  const auto t0 = std::chrono::steady_clock::now();
+  if (size_ > 1) {
+    Contig c(t);
+    shm().reduce(c.ptr(), t.numel(), t.scalar_type(), opts.reduceOp.op_, (int)opts.rootRank,
+                 eff_timeout(opts.timeout));
+    if (rank_ == opts.rootRank) c.write_back();
+  }
+  record(Coll::REDUCE, "shm", t.nbytes(), t0);
+  return cpu_done(Coll::REDUCE, tensors);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::broadcast(std::vector<at::Tensor>& tensors,
+                                                             const c10d::BroadcastOptions& opts) {
+  check_single(tensors, "broadcast");
+  check_root(opts.rootRank, size_, "broadcast");
+  at::Tensor& t = tensors[0];
+  before_op(Coll::BROADCAST, tensors, (int)opts.rootRank);
+  if (t.is_cuda()) return gpu_broadcast(t, (int)opts.rootRank, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  if (size_ > 1) {
+    Contig c(t);
+    shm().broadcast(c.ptr(), t.nbytes(), (int)opts.rootRank, eff_timeout(opts.timeout));
+    c.write_back();
+  }
+  record(Coll::BROADCAST, "shm", t.nbytes(), t0);
+  return cpu_done(Coll::BROADCAST, tensors);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather(std::vector<std::vector<at::Tensor>>& outputs,
+                                                             std::vector<at::Tensor>& inputs,
+                                                             const c10d::AllgatherOptions& opts) {
+  check_single(inputs, "allgather");
+  TORCH_CHECK(outputs.size() == 1, "ProcessGroupMI355X::allgather: expects one output list");
+  at::Tensor& in = inputs[0];
+  check_list(outputs[0], in, size_, "allgather", "output");
+  before_op(Coll::ALLGATHER, inputs, -1);
+  if (in.is_cuda()) return gpu_allgather(outputs[0], in, -1, false, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  Contig ci(in);
+  std::vector<Contig> co;
+  std::vector<void*> ptrs;
+  for (auto& o : outputs[0]) co.emplace_back(o);
+  for (auto& c : co) ptrs.push_back(c.ptr());
+  if (size_ > 1) shm().allgather(ci.ptr(), ptrs, in.nbytes(), eff_timeout(opts.timeout));
+  else std::memcpy(ptrs[0], ci.ptr(), in.nbytes());
+  for (auto& c : co) c.write_back();
+  record(Coll::ALLGATHER, "shm", in.nbytes(), t0);
+  return cpu_done(Coll::ALLGATHER, outputs[0]);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_allgather_base(at::Tensor& output, at::Tensor& input,
+                                                                   const c10d::AllgatherOptions& opts) {
+  TORCH_CHECK(output.numel() == input.numel() * size_, "ProcessGroupMI355X::_allgather_base: output has ",
+              output.numel(), " elements, expected ", input.numel() * size_);
+  TORCH_CHECK(output.scalar_type() == input.scalar_type(), "ProcessGroupMI355X::_allgather_base: dtype mismatch");
+  TORCH_CHECK(output.is_contiguous(), "ProcessGroupMI355X::_allgather_base: output must be contiguous");
+  std::vector<std::vector<at::Tensor>> outs(1);
+  auto flat = output.view({-1});
+  for (int r = 0; r < size_; ++r) outs[0].push_back(flat.narrow(0, r * input.numel(), input.numel()).view(input.sizes()));
+  std::vector<at::Tensor> ins{input};
+  return allgather(outs, ins, opts);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather_into_tensor_coalesced(std::vector<at::Tensor>& outputs,
+                                                                                   std::vector<at::Tensor>& inputs,
+                                                                                   const c10d::AllgatherOptions& opts) {
+  TORCH_CHECK(outputs.size() == inputs.size(), "allgather_into_tensor_coalesced: list size mismatch");
+  c10::intrusive_ptr<c10d::Work> last;
+  for (size_t i = 0; i < inputs.size(); ++i) last = _allgather_base(outputs[i], inputs[i], opts);
+  return last ? last : cpu_done(Coll::ALLGATHER, {});
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gather(std::vector<std::vector<at::Tensor>>& outputs,
+                                                          std::vector<at::Tensor>& inputs,
+                                                          const c10d::GatherOptions& opts) {
+  check_single(inputs, "gather");
+  check_root(opts.rootRank, size_, "gather");
+  at::Tensor& in = inputs[0];
+  const int root = (int)opts.rootRank;
+  if (rank_ == root) {
+    TORCH_CHECK(outputs.size() == 1, "ProcessGroupMI355X::gather: root expects one output list");
+    check_list(outputs[0], in, size_, "gather", "output");
+  } else {
+    TORCH_CHECK(outputs.empty() || outputs[0].empty(),
+                "ProcessGroupMI355X::gather: output list must be empty on non-root ranks");
+  }
+  before_op(Coll::GATHER, inputs, root);
+  std::vector<at::Tensor> empty;
+  std::vector<at::Tensor>& outl = (rank_ == root) ? outputs[0] : empty;
+  if (in.is_cuda()) return gpu_allgather(outl, in, root, true, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  Contig ci(in);
+  std::vector<Contig> co;
+  std::vector<void*> ptrs(size_, nullptr);
+  for (auto& o : outl) co.emplace_back(o);
+  for (size_t i = 0; i < co.size(); ++i) ptrs[i] = co[i].ptr();
+  if (size_ > 1) shm().gather(ci.ptr(), ptrs, in.nbytes(), root, eff_timeout(opts.timeout));
+  else std::memcpy(ptrs[0], ci.ptr(), in.nbytes());
+  for (auto& c : co) c.write_back();
+  record(Coll::GATHER, "shm", in.nbytes(), t0);
+  return cpu_done(Coll::GATHER, outl);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::scatter(std::vector<at::Tensor>& outputs,
+                                                           std::vector<std::vector<at::Tensor>>& inputs,
+                                                           const c10d::ScatterOptions& opts) {
+  check_single(outputs, "scatter");
+  check_root(opts.rootRank, size_, "scatter");
+  at::Tensor& out = outputs[0];
+  const int root = (int)opts.rootRank;
+  if (rank_ == root) {
+    TORCH_CHECK(inputs.size() == 1, "ProcessGroupMI355X::scatter: root expects one input list");
+    check_list(inputs[0], out, size_, "scatter", "input");
+  } else {
+    TORCH_CHECK(inputs.empty() || inputs[0].empty(),
+                "ProcessGroupMI355X::scatter: input list must be empty on non-root ranks");
+  }
+  before_op(Coll::SCATTER, outputs, root);
+  std::vector<at::Tensor> empty;
+  std::vector<at::Tensor>& inl = (rank_ == root) ? inputs[0] : empty;
+  if (out.is_cuda()) return gpu_scatter(out, inl, root, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<at::Tensor> ci;
+  std::vector<const void*> ptrs(size_, nullptr);
+  for (auto& i : inl) ci.push_back(i.contiguous());
+  for (size_t i = 0; i < ci.size(); ++i) ptrs[i] = ci[i].data_ptr();
+  Contig co(out);
+  if (size_ > 1) shm().scatter(ptrs, co.ptr(), out.nbytes(), root, eff_timeout(opts.timeout));
+  else std::memcpy(co.ptr(), ptrs[0], out.nbytes());
+  co.write_back();
+  record(Coll::SCATTER, "shm", out.nbytes(), t0);
+  return cpu_done(Coll::SCATTER, outputs);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter(std::vector<at::Tensor>& outputs,
+                                                                  std::vector<std::vector<at::Tensor>>& inputs,
+                                                                  const c10d::ReduceScatterOptions& opts) {
+  check_single(outputs, "reduce_scatter");
+  TORCH_CHECK(inputs.size() == 1, "ProcessGroupMI355X::reduce_scatter: expects one input list");
+  at::Tensor& out = outputs[0];
+  check_list(inputs[0], out, size_, "reduce_scatter", "input");
+  before_op(Coll::REDUCE_SCATTER, outputs, -1);
+  if (out.is_cuda()) return gpu_reduce_scatter(out, inputs[0], opts.reduceOp.op_, eff_timeout(opts.timeout));
+  check_cpu_dtype(out.scalar_type(), opts.reduceOp.op_, "reduce_scatter");
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<at::Tensor> ci;
+  std::vector<const void*> ptrs;
+  for (auto& i : inputs[0]) ci.push_back(i.contiguous());
+  for (auto& c : ci) ptrs.push_back(c.data_ptr());
+  Contig co(out);
+  if (size_ > 1)
+    shm().reduce_scatter(ptrs, co.ptr(), out.numel(), out.scalar_type(), opts.reduceOp.op_,
+                         eff_timeout(opts.timeout));
+  else
+    std::memcpy(co.ptr(), ptrs[0], out.nbytes());
+  co.write_back();
+  record(Coll::REDUCE_SCATTER, "shm", out.nbytes(), t0);
+  return cpu_done(Coll::REDUCE_SCATTER, outputs);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_reduce_scatter_base(at::Tensor& output, at::Tensor& input,
+                                                                        const c10d::ReduceScatterOptions& opts) {
+  TORCH_CHECK(input.numel() == output.numel() * size_, "ProcessGroupMI355X::_reduce_scatter_base: input has ",
+              input.numel(), " elements, expected ", output.numel() * size_);
+  TORCH_CHECK(input.is_contiguous(), "ProcessGroupMI355X::_reduce_scatter_base: input must be contiguous");
+  std::vector<std::vector<at::Tensor>> ins(1);
+  auto flat = input.view({-1});
+  for (int r = 0; r < size_; ++r) ins[0].push_back(flat.narrow(0, r * output.numel(), output.numel()).view(output.sizes()));
+  std::vector<at::Tensor> outs{output};
+  return reduce_scatter(outs, ins, opts);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter_tensor_coalesced(
+    std::vector<at::Tensor>& outputs, std::vector<at::Tensor>& inputs, const c10d::ReduceScatterOptions& opts) {
+  TORCH_CHECK(outputs.size() == inputs.size(), "reduce_scatter_tensor_coalesced: list size mismatch");
+  c10::intrusive_ptr<c10d::Work> last;
+  for (size_t i = 0; i < inputs.size(); ++i) last = _reduce_scatter_base(outputs[i], inputs[i], opts);
+  return last ? last : cpu_done(Coll::REDUCE_SCATTER, {});
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall_base(at::Tensor& output, at::Tensor& input,
+                                                                 std::vector<int64_t>& output_splits,
+                                                                 std::vector<int64_t>& input_splits,
+                                                                 const c10d::AllToAllOptions& opts) {
+  TORCH_CHECK(input.is_contiguous() && output.is_contiguous(), "ProcessGroupMI355X::alltoall_base: contiguous tensors only");
+  TORCH_CHECK(input.scalar_type() == output.scalar_type(), "ProcessGroupMI355X::alltoall_base: dtype mismatch");
+  const bool equal = output_splits.empty() && input_splits.empty();
+  auto split = [&](const at::Tensor& t, const std::vector<int64_t>& sp) {
+    std::vector<at::Tensor> v;
+    const int64_t rows = t.dim() == 0 ? 1 : t.size(0);
+    const int64_t row_el = rows == 0 ? 0 : t.numel() / rows;
+    auto flat = t.view({-1});
+    int64_t off = 0;
+    for (int r = 0; r < size_; ++r) {
+      const int64_t n = sp.empty() ? rows / size_ : sp[r];
+      v.push_back(flat.narrow(0, off * row_el, n * row_el));
+      off += n;
+    }
+    return v;
+  };
+  if (equal) {
+    const int64_t rows = input.dim() == 0 ? 1 : input.size(0);
+    TORCH_CHECK(rows % size_ == 0, "ProcessGroupMI355X::alltoall_base: dim 0 (", rows,
+                ") must be divisible by the group size (", size_, ")");
+    TORCH_CHECK(input.numel() == output.numel(), "ProcessGroupMI355X::alltoall_base: numel mismatch");
+  } else {
+    TORCH_CHECK((int)output_splits.size() == size_ && (int)input_splits.size() == size_,
+                "ProcessGroupMI355X::alltoall_base: split lists must have one entry per rank");
+  }
+  auto outs = split(output, output_splits);
+  auto ins = split(input, input_splits);
+  std::vector<at::Tensor> one{input};
+  before_op(Coll::ALLTOALL, one, -1);
+  if (input.is_cuda()) return gpu_alltoall(outs, ins, equal, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<const void*> ip;
+  std::vector<void*> op;
+  std::vector<size_t> sb, rb;
+  for (auto& t : ins) { ip.push_back(t.data_ptr()); sb.push_back(t.nbytes()); }
+  for (auto& t : outs) { op.push_back(t.data_ptr()); rb.push_back(t.nbytes()); }
+  if (size_ > 1) shm().alltoall(ip, sb, op, rb, eff_timeout(opts.timeout));
+  else std::memcpy(op[0], ip[0], sb[0]);
+  record(Coll::ALLTOALL, "shm", input.nbytes(), t0);
+  return cpu_done(Coll::ALLTOALL, {output});
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall(std::vector<at::Tensor>& outputs,
+                                                            std::vector<at::Tensor>& inputs,
+                                                            const c10d::AllToAllOptions& opts) {
+  TORCH_CHECK((int)outputs.size() == size_ && (int)inputs.size() == size_,
+              "ProcessGroupMI355X::alltoall: expects one input and one output tensor per rank");
+  before_op(Coll::ALLTOALL, inputs, -1);
+  if (inputs[0].is_cuda()) return gpu_alltoall(outputs, inputs, false, eff_timeout(opts.timeout));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<at::Tensor> ci;
+  std::vector<Contig> co;
+  std::vector<const void*> ip;
+  std::vector<void*> op;
+  std::vector<size_t> sb, rb;
+  size_t total = 0;
+  for (auto& t : inputs) { ci.push_back(t.contiguous()); }
+  for (auto& t : ci) { ip.push_back(t.data_ptr()); sb.push_back(t.nbytes()); total += t.nbytes(); }
+  for (auto& t : outputs) co.emplace_back(t);
+  for (size_t i = 0; i < co.size(); ++i) { op.push_back(co[i].ptr()); rb.push_back(outputs[i].nbytes()); }
+  if (size_ > 1) shm().alltoall(ip, sb, op, rb, eff_timeout(opts.timeout));
+  else std::memcpy(op[0], ip[0], sb[0]);
+  for (auto& c : co) c.write_back();
+  record(Coll::ALLTOALL, "shm", total, t0);
+  return cpu_done(Coll::ALLTOALL, outputs);
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::send(std::vector<at::Tensor>& tensors, int dst, int tag) {
+  check_single(tensors, "send");
+  TORCH_CHECK(dst >= 0 && dst < size_ && dst != rank_, "ProcessGroupMI355X::send: invalid destination rank ", dst);
+  before_op(Coll::SEND, tensors, dst);
+  at::Tensor t = tensors[0];
+  if (t.is_cuda()) return gpu_p2p(t, dst, true, timeout_);
+  at::Tensor c = t.contiguous();
+  auto work = c10::make_intrusive<WorkMI355X>(rank_, c10d::OpType::SEND, op_seq_.load(), std::vector<at::Tensor>{t});
+  auto to = timeout_;
+  host::ShmComm* sc = &shm();
+  p2p_submit(true, Job{[sc, c, dst, to] { sc->send(c.data_ptr(), c.nbytes(), dst, to); }, work});
+  if (coalescing_) coalesced_cpu_.push_back(work);
+  return work;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::recv(std::vector<at::Tensor>& tensors, int src, int tag) {
+  check_single(tensors, "recv");
+  TORCH_CHECK(src >= 0 && src < size_ && src != rank_, "ProcessGroupMI355X::recv: invalid source rank ", src);
+  before_op(Coll::RECV, tensors, src);
+  at::Tensor t = tensors[0];
+  if (t.is_cuda()) return gpu_p2p(t, src, false, timeout_);
+  auto work = c10::make_intrusive<WorkMI355X>(rank_, c10d::OpType::RECV, op_seq_.load(), std::vector<at::Tensor>{t});
+  auto to = timeout_;
+  host::ShmComm* sc = &shm();
+  p2p_submit(false, Job{[sc, t, src, to]() mutable {
+                          at::Tensor c = t.is_contiguous() ? t : at::empty_like(t, at::MemoryFormat::Contiguous);
+                          sc->recv(c.data_ptr(), c.nbytes(), src, to);
+                          if (!c.is_same(t)) t.copy_(c);
+                        },
+                        work});
+  if (coalescing_) coalesced_cpu_.push_back(work);
+  return work;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::barrier(const c10d::BarrierOptions& opts) {
+  before_op(Coll::BARRIER, {}, -1);
+  const auto t0 = std::chrono::steady_clock::now();
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    for (auto& kv : devs_) PDCC_HIP(hipStreamSynchronize(kv.second->stream.stream()));
+  }
+  if (size_ > 1) {
+    if (same_host_) shm().barrier(eff_timeout(opts.timeout));
+    else store_barrier(store_, "pdcc/barrier/" + std::to_string(op_seq_.load()), rank_, size_);
+  }
+  record(Coll::BARRIER, same_host_ ? "shm" : "store", 0, t0);
+  return cpu_done(Coll::BARRIER, {});
+}
+
+c10::intrusive_ptr<c10d::Backend> create_backend(const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
+                                                 std::chrono::milliseconds timeout, std::vector<int64_t> global_ranks,
+                                                 std::string group_name) {
+  return c10::make_intrusive<ProcessGroupMI355X>(store, rank, size, timeout, std::move(global_ranks),
+                                                 std::move(group_name));
+}
+
+}  // namespace pdcc

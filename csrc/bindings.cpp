@@ -1,0 +1,131 @@
+// Python bindings of the native library (module `_C` of the package).
+//  * ProcessGroupMI355X  -- the c10d backend (subclass of torch's Backend type)
+//  * kernel ops           -- K1 reduce_nway (LDS-DMA and register variants) and
+//                            K2 multi_copy on torch tensors, on the current stream
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+#include <pybind11/chrono.h>
+#include <pybind11/stl.h>
+#include <torch/csrc/utils/pybind.h>
+#include <torch/python.h>
+
+#include "backend/process_group.h"
+#include "device/comm_util.h"
+#include "kernels/kernel_api.h"
+
+namespace py = pybind11;
+
+namespace {
+
+pdcc::kern::DType kdtype(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return pdcc::kern::DType::F32;
+    case at::kHalf: return pdcc::kern::DType::F16;
+    case at::kBFloat16: return pdcc::kern::DType::BF16;
+    case at::kDouble: return pdcc::kern::DType::F64;
+    case at::kChar: return pdcc::kern::DType::I8;
+    case at::kByte: return pdcc::kern::DType::U8;
+    case at::kInt: return pdcc::kern::DType::I32;
+    case at::kLong: return pdcc::kern::DType::I64;
+    case at::kBool: return pdcc::kern::DType::BOOL;
+    default: TORCH_CHECK(false, "pdcc.ops: unsupported dtype ", t);
+  }
+}
+
+pdcc::kern::RedOp kop(const std::string& s) {
+  if (s == "sum") return pdcc::kern::RedOp::SUM;
+  if (s == "avg") return pdcc::kern::RedOp::AVG;
+  if (s == "prod" || s == "product") return pdcc::kern::RedOp::PROD;
+  if (s == "min") return pdcc::kern::RedOp::MIN;
+  if (s == "max") return pdcc::kern::RedOp::MAX;
+  if (s == "band") return pdcc::kern::RedOp::BAND;
+  if (s == "bor") return pdcc::kern::RedOp::BOR;
+  if (s == "bxor") return pdcc::kern::RedOp::BXOR;
+  TORCH_CHECK(false, "pdcc.ops: unknown reduce op '", s, "'");
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std::string& op, bool lds,
+                 int max_blocks) {
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= pdcc::kern::kMaxRanks, "reduce_nway: 1..8 sources");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && al16(out.data_ptr()), "reduce_nway: out must be a contiguous, "
+              "16-byte aligned GPU tensor");
+  std::vector<const void*> p;
+  for (const auto& s : srcs) {
+    TORCH_CHECK(s.device() == out.device() && s.scalar_type() == out.scalar_type() && s.numel() == out.numel() &&
+                    s.is_contiguous() && al16(s.data_ptr()),
+                "reduce_nway: sources must match out (device, dtype, numel) and be contiguous + 16-byte aligned");
+    p.push_back(s.data_ptr());
+  }
+  const auto k = kop(op);
+  const auto d = kdtype(out.scalar_type());
+  TORCH_CHECK(pdcc::kern::supports(d, k), "reduce_nway: op '", op, "' unsupported for ", out.scalar_type());
+  c10::hip::HIPGuard g(out.device());
+  hipStream_t s = c10::hip::getCurrentHIPStream(out.device().index()).stream();
+  hipError_t e = lds ? pdcc::kern::reduce_nway(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
+                                               (int)srcs.size(), s, max_blocks)
+                     : pdcc::kern::reduce_nway_regs(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
+                                                    (int)srcs.size(), s, max_blocks);
+  TORCH_CHECK(e == hipSuccess, "reduce_nway launch failed: ", hipGetErrorString(e));
+}
+
+void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "multi_copy: list length mismatch");
+  if (srcs.empty()) return;
+  std::vector<pdcc::kern::CopyDesc> d;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& a = srcs[i];
+    const auto& b = dsts[i];
+    TORCH_CHECK(a.is_cuda() && b.device() == a.device(), "multi_copy: tensors must be on one GPU");
+    TORCH_CHECK(a.nbytes() == b.nbytes(), "multi_copy: pair ", i, " size mismatch");
+    TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && al16(a.data_ptr()) && al16(b.data_ptr()),
+                "multi_copy: tensors must be contiguous and 16-byte aligned");
+    d.push_back({a.data_ptr(), b.data_ptr(), a.nbytes()});
+  }
+  c10::hip::HIPGuard g(srcs[0].device());
+  hipStream_t s = c10::hip::getCurrentHIPStream(srcs[0].device().index()).stream();
+  hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s);
+  TORCH_CHECK(e == hipSuccess, "multi_copy launch failed: ", hipGetErrorString(e));
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native collective communication backend (c10d) and gfx950 kernels";
+  py::module::import("torch.distributed");  // registers c10d::Backend / Store with pybind
+
+  py::class_<pdcc::ProcessGroupMI355X, c10d::Backend, c10::intrusive_ptr<pdcc::ProcessGroupMI355X>>(
+      m, "ProcessGroupMI355X")
+      .def(py::init([](const c10::intrusive_ptr<c10d::Store>& store, int rank, int size,
+                       std::chrono::milliseconds timeout, std::vector<int64_t> ranks, std::string name) {
+             return c10::make_intrusive<pdcc::ProcessGroupMI355X>(store, rank, size, timeout, std::move(ranks),
+                                                                  std::move(name));
+           }),
+           py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("timeout"),
+           py::arg("global_ranks") = std::vector<int64_t>{}, py::arg("group_name") = std::string(""),
+           py::call_guard<py::gil_scoped_release>())
+      .def("stats",
+           [](pdcc::ProcessGroupMI355X& pg) {
+             py::dict d;
+             for (const auto& kv : pg.stats())
+               d[py::str(kv.first)] = py::make_tuple(kv.second.calls, kv.second.bytes, kv.second.host_ms);
+             return d;
+           })
+      .def("reset_stats", &pdcc::ProcessGroupMI355X::reset_stats)
+      .def("describe", &pdcc::ProcessGroupMI355X::describe)
+      .def("last_algo", &pdcc::ProcessGroupMI355X::last_algo)
+      .def("healthy", &pdcc::ProcessGroupMI355X::healthy)
+      .def("health_message", &pdcc::ProcessGroupMI355X::health_message)
+      .def("set_algo", &pdcc::ProcessGroupMI355X::set_algo)
+      .def("set_ipc_thresholds", &pdcc::ProcessGroupMI355X::set_ipc_thresholds, py::arg("one_shot_max") = -1,
+           py::arg("two_shot_max") = -1, py::arg("copy_max") = -1)
+      .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>());
+
+  m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
+        py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");
+  m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), "K2: one-launch multi-tensor copy");
+  m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);
+  m.attr("MAX_RANKS_IPC") = pdcc::kern::kMaxRanks;
+  m.attr("TILE_BYTES") = pdcc::kern::kTileBytes;
+}

@@ -1,0 +1,70 @@
+// Peer-memory (hipIpc over xGMI) communicator: every rank owns
+//   * a staging buffer of 2 parities x `cap` bytes (coarse-grained HBM), and
+//   * a signal area (uncached device memory) holding the block-pairwise flags,
+// and maps every peer's staging + signal area into its own address space. The
+// IPC collective kernels (csrc/kernels) stage local data into the own buffer,
+// flag the peers, and pull/reduce straight out of the peers' buffers -- all 7
+// xGMI links of a node busy at once instead of one ring neighbour.
+//
+// Consecutive calls alternate parity, which makes an end-of-call barrier
+// unnecessary: before a rank writes a parity again, the start barrier of the
+// call in between proves every peer has finished the call that last read it.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <torch/csrc/distributed/c10d/Store.hpp>
+
+#include <string>
+#include <vector>
+
+#include "../kernels/kernel_api.h"
+
+namespace pdcc {
+
+class IpcComm {
+ public:
+  // Collective: allocate own signal area + error word and exchange handles.
+  IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world, int device,
+          size_t max_staging, uint64_t timeout_ms, bool shared_device);
+  ~IpcComm();
+  IpcComm(const IpcComm&) = delete;
+  IpcComm& operator=(const IpcComm&) = delete;
+
+  // Collective (all ranks pass the same value): grow the staging so one call of
+  // `bytes` fits. `stream` is drained before buffers are swapped.
+  void ensure_staging(size_t bytes, hipStream_t stream);
+  size_t max_staging() const { return max_staging_; }
+
+  // Launch one collective call (consumes one sequence number).
+  void launch(kern::IpcCall call, hipStream_t stream);
+
+  // Error word written by a kernel whose spin timed out (0 = healthy).
+  uint32_t error_word() const;
+  void clear_error();
+  bool shared_device() const { return shared_device_; }
+  int world() const { return world_; }
+  uint64_t calls() const { return seq_; }
+
+ private:
+  void map_staging(size_t cap);
+  void unmap_staging();
+
+  c10::intrusive_ptr<c10d::Store> store_;
+  std::string key_;
+  int rank_, world_, device_;
+  size_t max_staging_;
+  uint64_t timeout_ticks_;
+  bool shared_device_;
+
+  uint32_t* my_flags_ = nullptr;          // uncached device memory
+  std::vector<uint32_t*> peer_flags_;     // mapped (own entry = my_flags_)
+  uint32_t* err_host_ = nullptr;          // pinned, device-visible
+  uint32_t* err_dev_ = nullptr;
+
+  char* my_staging_ = nullptr;
+  size_t cap_ = 0;                         // bytes per parity
+  std::vector<char*> peer_staging_;
+  int staging_gen_ = 0;
+  uint32_t seq_ = 0;
+};
+
+}  // namespace pdcc

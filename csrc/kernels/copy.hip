@@ -1,0 +1,283 @@
+// K2 multi-tensor pack/unpack and the copy family of the IPC collectives
+// (broadcast, all-gather, gather, scatter, all-to-all, barrier), plus the
+// host-side entry points that dispatch on dtype into reduce_<dt>.hip.
+#include <algorithm>
+
+#include "reduce_impl.h"
+
+namespace pdcc {
+namespace dev {
+
+// --------------------------------------------------------------------------- K2
+struct CopyArgs {
+  kern::CopyDesc d[kern::kMaxCopyDescs];
+  uint64_t prefix[kern::kMaxCopyDescs + 1];  // prefix sums of FULL tiles per descriptor
+  int n;
+  int ntail;                                  // descriptors with a partial last tile
+  int tail_idx[kern::kMaxCopyDescs];
+};
+
+struct DescMap {
+  const CopyArgs* a;
+  size_t first, stride, total;
+  __device__ size_t count() const { return first < total ? (total - 1 - first) / stride + 1 : 0; }
+  __device__ void locate(size_t i, int& j, size_t& lt) const {
+    const size_t g = first + i * stride;
+    int lo = 0, hi = a->n - 1;  // last j with prefix[j] <= g  (uniform scalar search)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (a->prefix[mid] <= g) lo = mid; else hi = mid - 1;
+    }
+    j = lo;
+    lt = g - a->prefix[lo];
+  }
+  __device__ const char* src(int, size_t i) const {
+    int j; size_t lt; locate(i, j, lt);
+    return (const char*)a->d[j].src + lt * kTile;
+  }
+  __device__ char* dst(size_t i) const {
+    int j; size_t lt; locate(i, j, lt);
+    return (char*)a->d[j].dst + lt * kTile;
+  }
+  __device__ size_t valid(size_t) const { return kTile; }
+};
+
+__global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+  const DescMap m{&a, blockIdx.x, gridDim.x, a.prefix[a.n]};
+  pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+  // partial last tiles: one block each, bounded plain loads
+  for (int k = blockIdx.x; k < a.ntail; k += gridDim.x) {
+    const kern::CopyDesc& d = a.d[a.tail_idx[k]];
+    const size_t full = d.bytes / kTile * kTile;
+    const size_t off = full + (threadIdx.x >> 6) * kWaveBytes + (threadIdx.x & 63) * 16;
+    if (off < d.bytes) {
+      const uint32_t lim = (uint32_t)(d.bytes - off < 16 ? d.bytes - off : 16);
+      const char* s = (const char*)d.src + off;
+      char* o = (char*)d.dst + off;
+      if (lim == 16) *reinterpret_cast<uint4*>(o) = *reinterpret_cast<const uint4*>(s);
+      else store_partial(o, load_partial(s, lim), lim);
+    }
+  }
+}
+
+// ----------------------------------------------------------- IPC copy family
+__global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+  const size_t G = gridDim.x, b = blockIdx.x;
+  const int me = v.rank, W = v.world;
+  const uint32_t ph0 = v.seq * 2u, ph1 = v.seq * 2u + 1u;
+  char* mine = v.buf[me];
+  const size_t nt = pad_tiles(c.bytes) / kTile;
+  const size_t cpad = nt * kTile;
+
+  switch (c.coll) {
+    case IpcColl::BARRIER:
+      block_barrier(v, ph0);
+      return;
+    case IpcColl::BROADCAST_1SHOT: {
+      if (me == c.root) stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      if (me == c.root) return;
+      const OneSrcMap m{v.buf[c.root], (char*)c.out[0], c.bytes, b, G, nt};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      return;
+    }
+    case IpcColl::BROADCAST_2SHOT: {
+      // rows (t / W) belong to block row % G; tile t is owned by rank t % W
+      if (me == c.root)
+        for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[0], mine, c.bytes, q + W * b, W * G, nt);
+      block_barrier(v, ph0);
+      if (me != c.root) {  // phase 1: fetch my owned tiles from the root (one link each)
+        const OneSrcMap m{v.buf[c.root], mine, cpad, me + W * b, W * G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      block_barrier(v, ph1);
+      if (me == c.root) return;
+      for (int j = 0; j < W; ++j) {  // phase 2: every owner's tiles, over all links at once
+        const int q = (me + j) % W;
+        const OneSrcMap m{v.buf[q], (char*)c.out[0], c.bytes, q + W * b, W * G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      return;
+    }
+    case IpcColl::ALLGATHER:
+    case IpcColl::GATHER: {
+      stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      if (c.coll == IpcColl::GATHER && me != c.root) return;
+      for (int j = 0; j < W; ++j) {
+        const int q = (me + j) % W;
+        const OneSrcMap m{v.buf[q], (char*)c.out[q], c.bytes, b, G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      return;
+    }
+    case IpcColl::SCATTER: {
+      if (me == c.root)
+        for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      const OneSrcMap m{v.buf[c.root] + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      return;
+    }
+    case IpcColl::ALLTOALL: {
+      for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      for (int j = 0; j < W; ++j) {
+        const int q = (me + j) % W;
+        const OneSrcMap m{v.buf[q] + me * cpad, (char*)c.out[q], c.bytes, b, G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      return;
+    }
+    default:
+      return;
+  }
+}
+
+}  // namespace dev
+
+// =============================================================== host entry points
+namespace kern {
+
+bool supports(DType t, RedOp op) {
+  if (op == RedOp::COPY) return true;
+  const bool is_float = t == DType::F32 || t == DType::F16 || t == DType::BF16 || t == DType::F64;
+  const bool is_int = t == DType::I8 || t == DType::U8 || t == DType::I32 || t == DType::I64;
+  if (t == DType::BOOL) return op == RedOp::MAX || op == RedOp::MIN || op == RedOp::BAND || op == RedOp::BOR ||
+                               op == RedOp::BXOR || op == RedOp::SUM || op == RedOp::PROD;
+  if (is_float) return op == RedOp::SUM || op == RedOp::AVG || op == RedOp::PROD || op == RedOp::MIN ||
+                       op == RedOp::MAX;
+  return is_int;
+}
+
+// bool: SUM == logical OR == MAX, PROD == logical AND == MIN (ProcessGroupNCCL semantics)
+static void canon(DType& t, RedOp& op) {
+  if (t == DType::BOOL) {
+    t = DType::U8;
+    if (op == RedOp::SUM) op = RedOp::MAX;
+    if (op == RedOp::PROD) op = RedOp::MIN;
+  }
+}
+
+static hipError_t k1_dispatch(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
+                              int avg_div, hipStream_t stream, int max_blocks, bool lds) {
+  if (nsrc < 1 || nsrc > kMaxRanks || op == RedOp::COPY || !supports(t, op)) return hipErrorInvalidValue;
+  canon(t, op);
+  const size_t nbytes = count * dtype_size(t);
+  if (nbytes == 0) return hipSuccess;
+  const size_t tiles = nbytes / kTileBytes;
+  int grid = (int)std::min<size_t>(std::max<size_t>(tiles, 1), max_blocks > 0 ? (size_t)max_blocks : 1024);
+  using namespace dev;
+  switch (t) {
+    case DType::F32: return k1_dispatch_F32(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::F16: return k1_dispatch_F16(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::BF16: return k1_dispatch_BF16(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::F64: return k1_dispatch_F64(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::I8: return k1_dispatch_I8(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::U8: return k1_dispatch_U8(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::I32: return k1_dispatch_I32(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    case DType::I64: return k1_dispatch_I64(srcs, nsrc, out, nbytes, op, avg_div, stream, grid, lds);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t reduce_nway(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op, int avg_div,
+                       hipStream_t stream, int max_blocks) {
+  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, true);
+}
+hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
+                            int avg_div, hipStream_t stream, int max_blocks) {
+  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, false);
+}
+
+hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream) {
+  for (int base = 0; base < n; base += kMaxCopyDescs) {
+    dev::CopyArgs a{};
+    const int m = std::min(kMaxCopyDescs, n - base);
+    uint64_t acc = 0;
+    size_t bytes = 0;
+    for (int k = 0; k < m; ++k) {
+      a.d[a.n] = descs[base + k];
+      if (a.d[a.n].bytes == 0) continue;
+      a.prefix[a.n] = acc;
+      acc += a.d[a.n].bytes / kTileBytes;
+      if (a.d[a.n].bytes % kTileBytes) a.tail_idx[a.ntail++] = a.n;
+      bytes += a.d[a.n].bytes;
+      ++a.n;
+    }
+    if (a.n == 0) continue;
+    a.prefix[a.n] = acc;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), 1024));
+    hipLaunchKernelGGL(dev::k2_multi_copy, dim3(grid), dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+size_t ipc_signal_bytes() { return (size_t)kMaxBlocks * kMaxRanks * sizeof(uint32_t); }
+
+size_t ipc_staging_bytes(const IpcCall& c, int world) {
+  const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
+  switch (c.coll) {
+    case IpcColl::SCATTER:
+    case IpcColl::REDUCE_SCATTER:
+    case IpcColl::ALLTOALL:
+      return cpad * world;
+    case IpcColl::BARRIER:
+      return 0;
+    default:
+      return cpad;
+  }
+}
+
+hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream) {
+  IpcCall c = call;
+  if (v.world < 2 || v.world > kMaxRanks) return hipErrorInvalidValue;
+  const size_t nt = (c.bytes + kTileBytes - 1) / kTileBytes;
+  int grid = c.grid;
+  if (grid <= 0) {
+    size_t g;
+    switch (c.coll) {
+      case IpcColl::ALLREDUCE_2SHOT:
+      case IpcColl::REDUCE_2SHOT:
+      case IpcColl::BROADCAST_2SHOT:
+        g = (nt + v.world - 1) / v.world;  // rows
+        break;
+      case IpcColl::BARRIER:
+        g = 1;
+        break;
+      default:
+        g = nt;
+    }
+    grid = (int)std::max<size_t>(1, std::min<size_t>(g, 512));
+  }
+  if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
+  grid = std::min(grid, kMaxBlocks);
+  const bool reducing = c.coll == IpcColl::ALLREDUCE_1SHOT || c.coll == IpcColl::ALLREDUCE_2SHOT ||
+                        c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
+                        c.coll == IpcColl::REDUCE_SCATTER;
+  if (!reducing) {
+    hipLaunchKernelGGL(dev::k_ipc_copy, dim3(grid), dim3(256), 0, stream, v, c);
+    return hipGetLastError();
+  }
+  if (!supports(c.dtype, c.op)) return hipErrorInvalidValue;
+  canon(c.dtype, c.op);
+  using namespace dev;
+  switch (c.dtype) {
+    case DType::F32: return ipc_dispatch_F32(v, c, stream, grid);
+    case DType::F16: return ipc_dispatch_F16(v, c, stream, grid);
+    case DType::BF16: return ipc_dispatch_BF16(v, c, stream, grid);
+    case DType::F64: return ipc_dispatch_F64(v, c, stream, grid);
+    case DType::I8: return ipc_dispatch_I8(v, c, stream, grid);
+    case DType::U8: return ipc_dispatch_U8(v, c, stream, grid);
+    case DType::I32: return ipc_dispatch_I32(v, c, stream, grid);
+    case DType::I64: return ipc_dispatch_I64(v, c, stream, grid);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace kern
+}  // namespace pdcc

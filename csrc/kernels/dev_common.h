@@ -1,0 +1,358 @@
+// Device-side building blocks shared by every gfx950 kernel in this library.
+//
+//  * element traits + reduction functors (SUM/AVG/PROD/MIN/MAX/BAND/BOR/BXOR),
+//    bf16/f16 accumulate in f32 across ALL sources and round once;
+//  * `pipe_run`: the LDS-DMA streaming engine. Each wave64 moves 1 KiB per source
+//    per tile with `global_load_lds_dwordx4` into a DEPTH-deep ring in LDS, waits
+//    with a counted `s_waitcnt vmcnt(N)` (never 0 in steady state), reads its own
+//    lanes back with `ds_read_b128` (inline asm, so hipcc does not insert the
+//    conservative vmcnt(0) it emits before a ds_read that may alias an in-flight
+//    LDS-DMA) and stores 16 B per lane. Waves only read LDS they filled
+//    themselves, so the ring needs no workgroup barrier.
+//  * cross-GPU signalling (K4): system-scope release -> relaxed system-scope flag
+//    store into the peer's uncached signal area -> bounded relaxed poll -> ONE
+//    system-scope acquire (cdna_hip_programming.md §6 Guideline 16, lifted from
+//    agent to system scope because the consumer is another GPU over xGMI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "kernel_api.h"
+
+namespace pdcc {
+namespace dev {
+
+using kern::DType;
+using kern::RedOp;
+
+constexpr int kWaveBytes = 1024;  // 64 lanes x 16 B
+constexpr int kTile = kern::kTileBytes;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_cvoid_t;
+
+// ----------------------------------------------------------------------------
+// waits
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits on gfx9");
+  // gfx9 s_waitcnt simm16: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]
+  constexpr int enc = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+  __builtin_amdgcn_s_waitcnt(enc);
+}
+__device__ __forceinline__ void wait_lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(lds_void_t*)(p);
+}
+
+template <int IMM>
+__device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
+  uint4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(IMM));
+  return v;
+}
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// ----------------------------------------------------------------------------
+// element traits
+__device__ __forceinline__ float bf16_to_f32(uint16_t x) { return __uint_as_float((uint32_t)x << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // keep NaN a (quiet) NaN
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);                 // RNE
+}
+
+template <DType DT> struct Tr;
+template <> struct Tr<DType::F32> {
+  using S = float; using C = float; static constexpr bool kFloat = true;
+  __device__ static C in(S x) { return x; } __device__ static S out(C x) { return x; }
+};
+template <> struct Tr<DType::F64> {
+  using S = double; using C = double; static constexpr bool kFloat = true;
+  __device__ static C in(S x) { return x; } __device__ static S out(C x) { return x; }
+};
+template <> struct Tr<DType::F16> {
+  using S = _Float16; using C = float; static constexpr bool kFloat = true;
+  __device__ static C in(S x) { return (float)x; } __device__ static S out(C x) { return (_Float16)x; }
+};
+template <> struct Tr<DType::BF16> {
+  using S = uint16_t; using C = float; static constexpr bool kFloat = true;
+  __device__ static C in(S x) { return bf16_to_f32(x); } __device__ static S out(C x) { return f32_to_bf16(x); }
+};
+#define PDCC_INT_TR(DT, TYPE)                                                     \
+  template <> struct Tr<DT> {                                                     \
+    using S = TYPE; using C = TYPE; static constexpr bool kFloat = false;          \
+    __device__ static C in(S x) { return x; } __device__ static S out(C x) { return x; } \
+  };
+PDCC_INT_TR(DType::I8, int8_t)
+PDCC_INT_TR(DType::U8, uint8_t)
+PDCC_INT_TR(DType::I32, int32_t)
+PDCC_INT_TR(DType::I64, int64_t)
+#undef PDCC_INT_TR
+
+template <RedOp OP, class C>
+__device__ __forceinline__ C apply_op(C a, C b) {
+  if constexpr (OP == RedOp::SUM || OP == RedOp::AVG) return a + b;
+  else if constexpr (OP == RedOp::PROD) return a * b;
+  else if constexpr (OP == RedOp::MAX) return (a > b || a != a) ? a : b;  // NaN propagates
+  else if constexpr (OP == RedOp::MIN) return (a < b || a != a) ? a : b;
+  else if constexpr (OP == RedOp::BAND) return a & b;
+  else if constexpr (OP == RedOp::BOR) return a | b;
+  else if constexpr (OP == RedOp::BXOR) return a ^ b;
+  else return a;
+}
+
+// Reduce NSRC 16-byte vectors element-wise (sources combined in index order, so
+// every rank that runs the same reduction gets bit-identical results).
+template <DType DT, RedOp OP, int NSRC>
+__device__ __forceinline__ uint4 reduce_vec(const uint4 (&v)[NSRC], int avg_div) {
+  if constexpr (OP == RedOp::COPY) {
+    return v[0];
+  } else {
+    using T = Tr<DT>;
+    using S = typename T::S;
+    using C = typename T::C;
+    constexpr int N = 16 / sizeof(S);
+    S s[N];
+    C acc[N];
+    __builtin_memcpy(s, &v[0], 16);
+#pragma unroll
+    for (int e = 0; e < N; ++e) acc[e] = T::in(s[e]);
+#pragma unroll
+    for (int k = 1; k < NSRC; ++k) {
+      __builtin_memcpy(s, &v[k], 16);
+#pragma unroll
+      for (int e = 0; e < N; ++e) acc[e] = apply_op<OP, C>(acc[e], T::in(s[e]));
+    }
+    if constexpr (OP == RedOp::AVG) {
+#pragma unroll
+      for (int e = 0; e < N; ++e) acc[e] = acc[e] / (C)avg_div;
+    }
+#pragma unroll
+    for (int e = 0; e < N; ++e) s[e] = T::out(acc[e]);
+    uint4 r;
+    __builtin_memcpy(&r, s, 16);
+    return r;
+  }
+}
+
+// Store / load `lim` (< 16) leading bytes of a 16-B vector (buffer tails). Fully
+// unrolled on constant byte indices so nothing lands in scratch or LDS.
+__device__ __forceinline__ void store_partial(char* d, const uint4& r, uint32_t lim) {
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if ((uint32_t)j < lim) d[j] = (char)(w[j >> 2] >> (8 * (j & 3)));
+}
+__device__ __forceinline__ uint4 load_partial(const char* s, uint32_t lim) {
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+    if ((uint32_t)j < lim) w[j >> 2] |= (uint32_t)(uint8_t)s[j] << (8 * (j & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ----------------------------------------------------------------------------
+// LDS-DMA streaming engine.
+//
+// Map (per block) must provide:
+//   size_t count()                 tiles this block processes
+//   const char* src(int s, size_t i)   base of tile i in source s (tile is 4 KiB, fully readable)
+//   char* dst(size_t i)            base of tile i in the destination
+//   size_t valid(size_t i)         bytes of tile i that may be written (<= 4096)
+template <int NSRC, int DEPTH>
+struct PipeLds {
+  static constexpr int kBytes = DEPTH * NSRC * kTile;
+};
+
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
+__device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
+  static_assert((DEPTH - 1) * (NSRC + 1) < 64, "pipeline too deep for vmcnt");
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t lane_off = wave * kWaveBytes + lane * 16;
+  const size_t n = m.count();
+
+  auto issue = [&](size_t i, int stage) {
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s)
+      glds16(m.src(s, i) + lane_off, lds + (stage * NSRC + s) * kTile + wave * kWaveBytes);
+  };
+  auto consume = [&](size_t i, int stage) {
+    const uint32_t a = lds_off(lds + stage * NSRC * kTile + lane_off);
+    uint4 v[NSRC];
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) {
+      // offsets are compile-time immediates (s * 4096 < 64 KiB)
+      switch (s) {
+        case 0: v[s] = ds_read16<0 * kTile>(a); break;
+        case 1: v[s] = ds_read16<1 * kTile>(a); break;
+        case 2: v[s] = ds_read16<2 * kTile>(a); break;
+        case 3: v[s] = ds_read16<3 * kTile>(a); break;
+        case 4: v[s] = ds_read16<4 * kTile>(a); break;
+        case 5: v[s] = ds_read16<5 * kTile>(a); break;
+        case 6: v[s] = ds_read16<6 * kTile>(a); break;
+        default: v[s] = ds_read16<7 * kTile>(a); break;
+      }
+    }
+    wait_lgkm0();
+    const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
+    char* d = m.dst(i);
+    const size_t lim = m.valid(i);
+    if (lane_off + 16 <= lim) {
+      *reinterpret_cast<uint4*>(d + lane_off) = r;
+    } else if (lane_off < lim) {
+      store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
+    }
+  };
+
+#pragma unroll
+  for (int d = 0; d < DEPTH - 1; ++d)
+    if ((size_t)d < n) issue(d, d);
+  size_t i = 0;
+  int stage = 0;
+  for (; i + (DEPTH - 1) < n; ++i) {
+    int ns = stage + DEPTH - 1;
+    if (ns >= DEPTH) ns -= DEPTH;
+    issue(i + DEPTH - 1, ns);
+    // outstanding after tile i's loads: (DEPTH-1) younger tiles x NSRC loads
+    // plus one store per consumed tile in between
+    wait_vmcnt<(DEPTH - 1) * (NSRC + 1)>();
+    consume(i, stage);
+    stage = (stage + 1 == DEPTH) ? 0 : stage + 1;
+  }
+  for (; i < n; ++i) {
+    wait_vmcnt<0>();
+    consume(i, stage);
+    stage = (stage + 1 == DEPTH) ? 0 : stage + 1;
+  }
+}
+
+// Register-staged engine (same Map contract): UNROLL tiles of NSRC vectors in
+// VGPRs per lane, no LDS. Kept for the A/B measurement against pipe_run.
+template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map>
+__device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint32_t lane_off = wave * kWaveBytes + lane * 16;
+  const size_t n = m.count();
+  size_t i = 0;
+  for (; i + UNROLL <= n; i += UNROLL) {
+    uint4 v[UNROLL][NSRC];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int s = 0; s < NSRC; ++s)
+        v[u][s] = *reinterpret_cast<const uint4*>(m.src(s, i + u) + lane_off);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint4 r = reduce_vec<DT, OP, NSRC>(v[u], avg_div);
+      char* d = m.dst(i + u);
+      const size_t lim = m.valid(i + u);
+      if (lane_off + 16 <= lim) *reinterpret_cast<uint4*>(d + lane_off) = r;
+      else if (lane_off < lim) store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
+    }
+  }
+  for (; i < n; ++i) {
+    uint4 v[NSRC];
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) v[s] = *reinterpret_cast<const uint4*>(m.src(s, i) + lane_off);
+    const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
+    char* d = m.dst(i);
+    const size_t lim = m.valid(i);
+    if (lane_off + 16 <= lim) *reinterpret_cast<uint4*>(d + lane_off) = r;
+    else if (lane_off < lim) store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
+  }
+}
+
+// Bounded local copy of the tiles {first, first+stride, ...} < ntiles of a user
+// buffer (nbytes long, 16-B aligned) into a padded staging buffer. Plain 16-B
+// loads (never LDS-DMA: reading past the end of a user allocation could fault).
+__device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* __restrict__ dst,
+                                            size_t nbytes, size_t first, size_t stride,
+                                            size_t ntiles) {
+  const uint32_t lane_off = (threadIdx.x >> 6) * kWaveBytes + (threadIdx.x & 63) * 16;
+  constexpr int U = 4;
+  size_t t = first;
+  for (; t + (U - 1) * stride < ntiles; t += U * stride) {
+    uint4 v[U];
+    size_t off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      off[u] = (t + u * stride) * kTile + lane_off;
+      v[u] = (off[u] + 16 <= nbytes) ? *reinterpret_cast<const uint4*>(src + off[u])
+             : (off[u] < nbytes ? load_partial(src + off[u], (uint32_t)(nbytes - off[u]))
+                                : make_uint4(0, 0, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) *reinterpret_cast<uint4*>(dst + off[u]) = v[u];
+  }
+  for (; t < ntiles; t += stride) {
+    const size_t off = t * kTile + lane_off;
+    uint4 v = (off + 16 <= nbytes) ? *reinterpret_cast<const uint4*>(src + off)
+              : (off < nbytes ? load_partial(src + off, (uint32_t)(nbytes - off)) : make_uint4(0, 0, 0, 0));
+    *reinterpret_cast<uint4*>(dst + off) = v;
+  }
+}
+
+// ----------------------------------------------------------------------------
+// K4: cross-GPU block-pairwise barrier.
+//
+// flags layout (per rank, uncached device memory): flags[block * kMaxRanks + src].
+// Values are monotonic (seq*2 for phase 0, seq*2+1 for phase 1), compared with a
+// wrap-safe signed difference, so flags never need re-zeroing and a fast peer
+// that already moved on never deadlocks a slow one.
+__device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
+  return (int32_t)(have - want) >= 0;
+}
+
+// Every wave of the block calls this after its last store of data that peers
+// will read. Returns false on timeout (error word set, block continues so the
+// grid always drains).
+__device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t value) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  drain_vm();       // every storing wave drains its stores
+  __syncthreads();  // ... before wave 0 publishes for the whole block
+  bool ok = true;
+  if (wave == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
+    drain_vm();                                     // keep the wait after the fence (G16 pitfall 12)
+    const int b = blockIdx.x;
+    if (lane < v.world) {
+      uint32_t* f = v.flags[lane] + b * kern::kMaxRanks + v.rank;
+      __hip_atomic_store(f, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const uint32_t* mine = v.flags[v.rank] + b * kern::kMaxRanks;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      bool me_ok = true;
+      if (lane < v.world)
+        me_ok = reached(__hip_atomic_load(mine + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), value);
+      if (__all(me_ok)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+        if (lane == 0)
+          __hip_atomic_store(v.err, 0x100u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
+    drain_vm();
+  }
+  __syncthreads();
+  return ok;
+}
+
+}  // namespace dev
+}  // namespace pdcc

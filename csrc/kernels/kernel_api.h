@@ -1,0 +1,119 @@
+// Host-visible launch API of the gfx950 HIP kernels (no torch headers here, so
+// the .hip translation units stay small and compile in parallel).
+//
+// Kernel inventory:
+//   K1  reduce_nway      out = Op(src_0 .. src_{k-1}), LDS-DMA staged tiles
+//   K2  multi_copy       pack / unpack a list of tensors <-> one staging buffer
+//   K3  peer pull        (inside the IPC collectives) xGMI reads of peer buffers
+//   K4  cross-GPU flags  (inside the IPC collectives) system-scope signal words
+//
+// The reference (main.py:14,23,37,52,68,81) calls the six torch.distributed
+// primitives on CPU/Gloo; these kernels are what the GPU path of this library
+// runs underneath the same calls.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pdcc {
+namespace kern {
+
+constexpr int kMaxRanks = 8;        // one xGMI-connected MI355X node
+constexpr int kMaxBlocks = 1024;    // per-block pairwise flags in the signal area
+constexpr int kTileBytes = 4096;    // 256 lanes x 16 B: the unit every engine moves
+constexpr int kBlockThreads = 256;  // 4 wave64s
+
+enum class DType : int32_t { F32 = 0, F16, BF16, F64, I8, U8, I32, I64, BOOL, kCount };
+enum class RedOp : int32_t { SUM = 0, AVG, PROD, MIN, MAX, BAND, BOR, BXOR, COPY, kCount };
+
+inline size_t dtype_size(DType t) {
+  switch (t) {
+    case DType::F32: return 4;
+    case DType::F16: return 2;
+    case DType::BF16: return 2;
+    case DType::F64: return 8;
+    case DType::I8: return 1;
+    case DType::U8: return 1;
+    case DType::I32: return 4;
+    case DType::I64: return 8;
+    case DType::BOOL: return 1;
+    default: return 0;
+  }
+}
+
+// true iff the (dtype, op) pair has a device kernel
+bool supports(DType t, RedOp op);
+
+// ---------------------------------------------------------------- K1
+// out[i] = Op(srcs[0][i], ..., srcs[nsrc-1][i]), 1 <= nsrc <= kMaxRanks.
+// AVG divides by `avg_div` (float types: multiply by 1/avg_div).
+// All pointers must be 16-byte aligned; count is in elements.
+hipError_t reduce_nway(const void* const* srcs, int nsrc, void* out, size_t count, DType t,
+                       RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0);
+
+// register-staged variant of K1 (same numerics) kept for A/B measurement
+hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t count, DType t,
+                            RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0);
+
+// ---------------------------------------------------------------- K2
+struct CopyDesc {
+  const void* src;
+  void* dst;
+  size_t bytes;
+};
+constexpr int kMaxCopyDescs = 64;  // per launch (kernarg); host splits longer lists
+// One launch copies every descriptor (pack = many->one, unpack = one->many).
+hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream);
+
+// ---------------------------------------------------------------- IPC collectives
+// Per-rank view of the group's registered (hipIpc) memory for ONE call.
+struct IpcView {
+  char* buf[kMaxRanks];        // staging buffer of this call's parity, per rank (own included)
+  uint32_t* flags[kMaxRanks];  // signal area (uncached device memory) per rank
+  uint32_t* err;               // host-mapped error word (0 = ok), written on spin timeout
+  int rank;
+  int world;
+  uint32_t seq;                // call sequence number (>= 1), identical on every rank
+  uint32_t pad_;
+  uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
+};
+
+enum class IpcColl : int32_t {
+  ALLREDUCE_1SHOT = 0,   // stage, barrier, every rank reduces everything from all peers
+  ALLREDUCE_2SHOT,       // stage, barrier, reduce own 1/W, barrier, gather the other W-1
+  REDUCE_1SHOT,          // stage, barrier, root reduces everything
+  REDUCE_2SHOT,          // reduce-scatter, barrier, root gathers
+  BROADCAST_1SHOT,       // root stages, barrier, everyone pulls from root
+  BROADCAST_2SHOT,       // scatter from root, barrier, all-gather among all
+  ALLGATHER,             // stage, barrier, pull W chunks
+  GATHER,                // stage, barrier, root pulls W chunks
+  SCATTER,               // root stages W chunks, barrier, rank r pulls chunk r
+  REDUCE_SCATTER,        // stage W chunks, barrier, rank r reduces chunk r
+  ALLTOALL,              // stage W chunks, barrier, rank r pulls chunk r of every peer
+  BARRIER,               // flags only
+  kCount
+};
+
+// Arguments of one IPC collective. `chunk_bytes` is the per-rank payload of one
+// chunk (all-gather/scatter/... operate on W chunks of that size).
+struct IpcCall {
+  IpcColl coll;
+  DType dtype;
+  RedOp op;
+  int root;
+  int avg_div;
+  int grid;                      // 0 = pick
+  int grid_cap;                  // > 0: upper bound on the picked grid (co-residency on shared devices)
+  size_t bytes;                  // payload bytes (per rank / per chunk, see above)
+  const void* in[kMaxRanks];     // local inputs: in[0] for single-tensor inputs, in[c] per chunk for lists
+  void* out[kMaxRanks];          // local outputs: out[0] single, out[c] per chunk for lists
+};
+
+// Bytes of staging needed per parity for `call` (padded to tiles).
+size_t ipc_staging_bytes(const IpcCall& call, int world);
+// Bytes of the signal area every rank must allocate (uncached memory).
+size_t ipc_signal_bytes();
+hipError_t ipc_launch(const IpcView& view, const IpcCall& call, hipStream_t stream);
+
+}  // namespace kern
+}  // namespace pdcc

@@ -1,0 +1,249 @@
+// K1 (standalone N-way reduce) and the reduction family of the IPC collectives,
+// templated on (dtype, op, #sources). Included once per dtype by reduce_<dt>.hip,
+// which instantiates PDCC_REDUCE_DTYPE(<dt>) -- 8 small TUs that hipcc builds in
+// parallel instead of one huge one.
+#pragma once
+#include "dev_common.h"
+
+namespace pdcc {
+namespace dev {
+
+using kern::IpcCall;
+using kern::IpcColl;
+using kern::IpcView;
+
+struct Ptrs8 {
+  const char* p[kern::kMaxRanks];
+};
+
+// LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU)
+template <int NSRC>
+struct DepthFor {
+  static constexpr int value = NSRC <= 2 ? 4 : (NSRC <= 4 ? 3 : 2);
+};
+
+// --------------------------------------------------------------------------- K1
+struct StridedMap {
+  const char* const* s;
+  char* d;
+  size_t first, stride, ntiles;
+  __device__ size_t count() const { return first < ntiles ? (ntiles - 1 - first) / stride + 1 : 0; }
+  __device__ size_t tile(size_t i) const { return first + i * stride; }
+  __device__ const char* src(int k, size_t i) const { return s[k] + tile(i) * kTile; }
+  __device__ char* dst(size_t i) const { return d + tile(i) * kTile; }
+  __device__ size_t valid(size_t) const { return kTile; }
+};
+
+// tail (< 4 KiB past the last full tile) with plain bounded loads
+template <DType DT, RedOp OP, int NSRC>
+__device__ __forceinline__ void reduce_tail(const char* const* s, char* d, size_t nbytes, int avg_div) {
+  const size_t full = (nbytes / kTile) * kTile;
+  const size_t off = full + (threadIdx.x >> 6) * kWaveBytes + (threadIdx.x & 63) * 16;
+  if (off >= nbytes) return;
+  const uint32_t lim = (uint32_t)(nbytes - off < 16 ? nbytes - off : 16);
+  uint4 v[NSRC];
+#pragma unroll
+  for (int k = 0; k < NSRC; ++k)
+    v[k] = lim == 16 ? *reinterpret_cast<const uint4*>(s[k] + off) : load_partial(s[k] + off, lim);
+  const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
+  if (lim == 16) *reinterpret_cast<uint4*>(d + off) = r;
+  else store_partial(d + off, r, lim);
+}
+
+template <DType DT, RedOp OP, int NSRC>
+__global__ void __launch_bounds__(256) k1_reduce_lds(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
+  constexpr int D = DepthFor<NSRC>::value;
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<NSRC, D>::kBytes];
+  const StridedMap m{srcs.p, dst, blockIdx.x, gridDim.x, nbytes / kTile};
+  pipe_run<DT, OP, NSRC, D>(lds, m, avg_div);
+  if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
+}
+
+template <DType DT, RedOp OP, int NSRC>
+__global__ void __launch_bounds__(256) k1_reduce_regs(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
+  const StridedMap m{srcs.p, dst, blockIdx.x, gridDim.x, nbytes / kTile};
+  pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2)>(m, avg_div);
+  if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
+}
+
+// ------------------------------------------------------------- IPC reductions
+// Tile partitions (MUST be identical on every rank: a block only ever reads
+// tiles that the same-index block of each peer staged, which is what makes the
+// block-pairwise barrier sufficient):
+//   1-shot / reduce-scatter: tile t (within a chunk) -> block t % G
+//   2-shot: tile t -> owner t % W, row t / W -> block row % G
+__device__ __forceinline__ size_t pad_tiles(size_t b) { return (b + kTile - 1) / kTile * kTile; }
+
+template <int W>
+struct AllSrcMap {  // reduce tile t of every rank's staging (+ chunk offset)
+  const IpcView* v;
+  size_t base;   // byte offset of the chunk inside each staging buffer
+  char* d;       // destination (user output or own staging)
+  size_t dlim;   // bytes writable at d (user: payload bytes; staging: padded)
+  size_t first, stride, ntiles;
+  __device__ size_t count() const { return first < ntiles ? (ntiles - 1 - first) / stride + 1 : 0; }
+  __device__ size_t tile(size_t i) const { return first + i * stride; }
+  __device__ const char* src(int k, size_t i) const { return v->buf[k] + base + tile(i) * kTile; }
+  __device__ char* dst(size_t i) const { return d + tile(i) * kTile; }
+  __device__ size_t valid(size_t i) const {
+    const size_t o = tile(i) * kTile;
+    return o >= dlim ? 0 : (dlim - o < (size_t)kTile ? dlim - o : (size_t)kTile);
+  }
+};
+
+struct OneSrcMap {  // copy tile t from one buffer to another
+  const char* s;
+  char* d;
+  size_t dlim;
+  size_t first, stride, ntiles;
+  __device__ size_t count() const { return first < ntiles ? (ntiles - 1 - first) / stride + 1 : 0; }
+  __device__ size_t tile(size_t i) const { return first + i * stride; }
+  __device__ const char* src(int, size_t i) const { return s + tile(i) * kTile; }
+  __device__ char* dst(size_t i) const { return d + tile(i) * kTile; }
+  __device__ size_t valid(size_t i) const {
+    const size_t o = tile(i) * kTile;
+    return o >= dlim ? 0 : (dlim - o < (size_t)kTile ? dlim - o : (size_t)kTile);
+  }
+};
+
+constexpr int kCopyDepth = 4;
+
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
+  constexpr int D = DepthFor<W>::value;
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, D>::kBytes];
+  const size_t G = gridDim.x, b = blockIdx.x;
+  const int me = v.rank;
+  const uint32_t ph0 = v.seq * 2u, ph1 = v.seq * 2u + 1u;
+  char* mine = v.buf[me];
+  const size_t nt = pad_tiles(c.bytes) / kTile;
+
+  switch (c.coll) {
+    case IpcColl::ALLREDUCE_1SHOT:
+    case IpcColl::REDUCE_1SHOT: {
+      stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      if (c.coll == IpcColl::REDUCE_1SHOT && me != c.root) return;
+      const AllSrcMap<W> m{&v, 0, (char*)c.out[0], c.bytes, b, G, nt};
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      return;
+    }
+    case IpcColl::ALLREDUCE_2SHOT:
+    case IpcColl::REDUCE_2SHOT: {
+      // stage the rows of this block: tiles q + W*(b + G*k) for every owner q
+      for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[0], mine, c.bytes, q + W * b, W * G, nt);
+      block_barrier(v, ph0);
+      // phase 1: reduce my owned tiles from every rank, in place into my staging
+      {
+        const AllSrcMap<W> m{&v, 0, mine, nt * kTile, me + W * b, W * G, nt};
+        pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      }
+      block_barrier(v, ph1);
+      if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
+      // phase 2: pull every owner's reduced tiles (rotated start balances links)
+      for (int j = 0; j < W; ++j) {
+        const int q = (me + j) % W;
+        const OneSrcMap m{v.buf[q], (char*)c.out[0], c.bytes, q + W * b, W * G, nt};
+        pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      return;
+    }
+    case IpcColl::REDUCE_SCATTER: {
+      const size_t cpad = pad_tiles(c.bytes);
+      for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
+      block_barrier(v, ph0);
+      const AllSrcMap<W> m{&v, me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      return;
+    }
+    default:
+      return;
+  }
+}
+
+// host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)
+#define PDCC_DECL_DISPATCH(DTNAME)                                                                   \
+  hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,    \
+                                  int avg_div, hipStream_t s, int grid, bool lds);                   \
+  hipError_t ipc_dispatch_##DTNAME(const IpcView& v, const IpcCall& c, hipStream_t s, int grid);
+PDCC_DECL_DISPATCH(F32)
+PDCC_DECL_DISPATCH(F16)
+PDCC_DECL_DISPATCH(BF16)
+PDCC_DECL_DISPATCH(F64)
+PDCC_DECL_DISPATCH(I8)
+PDCC_DECL_DISPATCH(U8)
+PDCC_DECL_DISPATCH(I32)
+PDCC_DECL_DISPATCH(I64)
+#undef PDCC_DECL_DISPATCH
+
+template <DType DT, RedOp OP, int NSRC>
+hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_div, hipStream_t s, int grid,
+                     bool lds) {
+  Ptrs8 p{};
+  for (int k = 0; k < NSRC; ++k) p.p[k] = (const char*)srcs[k];
+  if (lds)
+    hipLaunchKernelGGL((k1_reduce_lds<DT, OP, NSRC>), dim3(grid), dim3(256), 0, s, p, (char*)out, nbytes, avg_div);
+  else
+    hipLaunchKernelGGL((k1_reduce_regs<DT, OP, NSRC>), dim3(grid), dim3(256), 0, s, p, (char*)out, nbytes, avg_div);
+  return hipGetLastError();
+}
+
+template <DType DT, RedOp OP>
+hipError_t k1_by_n(const void* const* srcs, int n, void* out, size_t nbytes, int avg_div, hipStream_t s, int grid,
+                   bool lds) {
+  switch (n) {
+    case 1: return launch_k1<DT, OP, 1>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 2: return launch_k1<DT, OP, 2>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 3: return launch_k1<DT, OP, 3>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 4: return launch_k1<DT, OP, 4>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 5: return launch_k1<DT, OP, 5>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 6: return launch_k1<DT, OP, 6>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 7: return launch_k1<DT, OP, 7>(srcs, out, nbytes, avg_div, s, grid, lds);
+    case 8: return launch_k1<DT, OP, 8>(srcs, out, nbytes, avg_div, s, grid, lds);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <DType DT, RedOp OP>
+hipError_t ipc_by_w(const IpcView& v, const IpcCall& c, hipStream_t s, int grid) {
+  switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL((k_ipc_reduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
+    PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace pdcc
+
+// Instantiate the dispatchers for one dtype. Float types get SUM/AVG/PROD/MIN/MAX,
+// integer types additionally BAND/BOR/BXOR.
+#define PDCC_OPS_FLOAT(F, ...) \
+  case RedOp::SUM: return F<DT, RedOp::SUM>(__VA_ARGS__); \
+  case RedOp::AVG: return F<DT, RedOp::AVG>(__VA_ARGS__); \
+  case RedOp::PROD: return F<DT, RedOp::PROD>(__VA_ARGS__); \
+  case RedOp::MIN: return F<DT, RedOp::MIN>(__VA_ARGS__); \
+  case RedOp::MAX: return F<DT, RedOp::MAX>(__VA_ARGS__);
+#define PDCC_OPS_INT(F, ...)              \
+  PDCC_OPS_FLOAT(F, __VA_ARGS__)          \
+  case RedOp::BAND: return F<DT, RedOp::BAND>(__VA_ARGS__); \
+  case RedOp::BOR: return F<DT, RedOp::BOR>(__VA_ARGS__); \
+  case RedOp::BXOR: return F<DT, RedOp::BXOR>(__VA_ARGS__);
+
+#define PDCC_REDUCE_DTYPE(DTNAME, OPSET)                                                              \
+  namespace pdcc {                                                                                    \
+  namespace dev {                                                                                     \
+  hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,     \
+                                  int avg_div, hipStream_t s, int grid, bool lds) {                   \
+    constexpr DType DT = DType::DTNAME;                                                               \
+    switch (op) { OPSET(k1_by_n, srcs, n, out, nb, avg_div, s, grid, lds) default: return hipErrorInvalidValue; } \
+  }                                                                                                   \
+  hipError_t ipc_dispatch_##DTNAME(const IpcView& v, const IpcCall& c, hipStream_t s, int grid) {     \
+    constexpr DType DT = DType::DTNAME;                                                               \
+    switch (c.op) { OPSET(ipc_by_w, v, c, s, grid) default: return hipErrorInvalidValue; }            \
+  }                                                                                                   \
+  }                                                                                                   \
+  }

@@ -1,0 +1,177 @@
+"""In-tree native build: gfx950 HIP kernels + C++ backend -> ``_C*.so``.
+
+Explicit ``hipcc``/``g++`` command lines (no hipify, no JIT cache): the kernels
+in ``csrc/kernels/*.hip`` are compiled for ``--offload-arch=gfx950`` only, the
+host C++ (c10d backend, shm transport, RCCL/IPC communicators, bindings) with
+``g++`` against the torch headers, and everything is linked against torch's own
+bundled HIP/RCCL (``torch/lib``) so the extension binds to the same runtime
+torch already loaded (SURVEY.md §7.1 "runtime duality").
+
+Usage: ``python -m pytorch_distributed_collective_communication_amd._build [-j N] [--force]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "obj")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PDCC_ARCH", "gfx950")
+
+
+def ext_path() -> str:
+    return os.path.join(PKG_DIR, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _torch_dirs():
+    import torch
+
+    tdir = os.path.dirname(torch.__file__)
+    return tdir, os.path.join(tdir, "include"), os.path.join(tdir, "lib")
+
+
+def _hipcc() -> str:
+    p = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    if not os.path.exists(p):
+        raise RuntimeError("hipcc not found (ROCm toolchain required to build the gfx950 kernels)")
+    return p
+
+
+def _sources():
+    hip = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    cpp = sorted(
+        glob.glob(os.path.join(CSRC, "host", "*.cpp"))
+        + glob.glob(os.path.join(CSRC, "device", "*.cpp"))
+        + glob.glob(os.path.join(CSRC, "backend", "*.cpp"))
+        + [os.path.join(CSRC, "bindings.cpp")]
+    )
+    return hip, cpp
+
+
+def _headers_mtime(sub: str) -> float:
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    if sub == "kernels":
+        hs = [h for h in hs if os.sep + "kernels" + os.sep in h]
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _obj(src: str) -> str:
+    rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
+    return os.path.join(BUILD, rel + ".o")
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build step failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+    return r.stdout
+
+
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> str:
+    """Compile (incrementally) and link the extension; returns the .so path."""
+    tdir, tinc, tlib = _torch_dirs()
+    import torch
+
+    os.makedirs(BUILD, exist_ok=True)
+    hip_srcs, cpp_srcs = _sources()
+    py_inc = sysconfig.get_paths()["include"]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    common_defs = [
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DUSE_ROCM=1",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DTORCH_EXTENSION_NAME=_C",
+        "-DTORCH_API_INCLUDE_EXTENSION_H",
+    ]
+    incs = [
+        f"-I{CSRC}",
+        f"-I{tinc}",
+        f"-I{os.path.join(tinc, 'torch', 'csrc', 'api', 'include')}",
+        f"-I{py_inc}",
+        f"-I{os.path.join(ROCM, 'include')}",
+    ]
+    hipcc = _hipcc()
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    kern_hdr = _headers_mtime("kernels")
+    all_hdr = _headers_mtime("all")
+
+    def stale(src, obj, hdr):
+        if force or not os.path.exists(obj):
+            return True
+        t = os.path.getmtime(obj)
+        return t < os.path.getmtime(src) or t < hdr
+
+    tasks = []
+    for s in hip_srcs:
+        o = _obj(s)
+        if stale(s, o, kern_hdr):
+            tasks.append(
+                [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-c", s, "-o", o]
+            )
+    for s in cpp_srcs:
+        o = _obj(s)
+        if stale(s, o, all_hdr):
+            tasks.append(
+                ["g++", "-O2", "-g0", "-fPIC", "-std=c++17", "-Wno-deprecated-declarations", "-Wno-attributes"]
+                + common_defs
+                + incs
+                + ["-c", s, "-o", o]
+            )
+    if tasks:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_run, t, verbose) for t in tasks]
+            for f in futs:
+                f.result()
+
+    objs = [_obj(s) for s in hip_srcs + cpp_srcs]
+    out = ext_path()
+    if force or tasks or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        link = (
+            ["g++", "-shared", "-o", out + ".tmp"]
+            + objs
+            + [
+                f"-L{tlib}",
+                f"-L{os.path.join(ROCM, 'lib')}",
+                "-lc10",
+                "-lc10_hip",
+                "-ltorch",
+                "-ltorch_cpu",
+                "-ltorch_hip",
+                "-ltorch_python",
+                f"-Wl,-rpath,{tlib}",
+                # torch's bundled runtime first: the extension must bind to the HIP/RCCL torch loaded
+                os.path.join(tlib, "libamdhip64.so"),
+                os.path.join(tlib, "librccl.so"),
+                "-lrt",
+                "-lpthread",
+                "-ldl",
+            ]
+        )
+        _run(link, verbose)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    p = build(a.jobs, a.force, a.verbose)
+    print(p)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,295 @@
+"""Per-rank worker functions for the multi-process tests (picklable by name).
+
+Each returns plain Python data; the test process compares it with the golden
+values of the reference (README.md:105-284 outputs).
+"""
+from __future__ import annotations
+
+import os
+import time
+
+
+def _dev(device: str):
+    import torch
+
+    if device == "cpu":
+        return torch.device("cpu")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def golden(rank, size, device="cpu", subgroup=True):
+    """The six primitives exactly as the reference calls them (main.py:9-83)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    g = dist.new_group(list(range(size))) if subgroup else None
+    out = {}
+    t = torch.ones(1, device=d)
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM, group=g)
+    out["reduce"] = t.cpu().tolist()
+    t = torch.ones(1, device=d)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
+    out["all_reduce"] = t.cpu().tolist()
+    t = torch.empty(1, device=d)
+    if rank == 0:
+        dist.scatter(t, scatter_list=[torch.tensor([i + 1.0], device=d) for i in range(size)], src=0, group=g)
+    else:
+        dist.scatter(t, scatter_list=[], src=0, group=g)
+    out["scatter"] = t.cpu().tolist()
+    t = torch.tensor([float(rank)], device=d)
+    if rank == 0:
+        lst = [torch.empty(1, device=d) for _ in range(size)]
+        dist.gather(t, gather_list=lst, dst=0, group=g)
+        out["gather"] = [x.item() for x in lst]
+    else:
+        dist.gather(t, gather_list=[], dst=0, group=g)
+    lst = [torch.empty(1, device=d) for _ in range(size)]
+    dist.all_gather(lst, torch.tensor([float(rank)], device=d), group=g)
+    out["all_gather"] = [x.item() for x in lst]
+    t = torch.tensor([0.0], device=d) if rank == 0 else torch.empty(1, device=d)
+    dist.broadcast(t, src=0, group=g)
+    out["broadcast"] = t.cpu().tolist()
+    return out
+
+
+def expected_golden(rank, size):
+    e = {
+        "all_reduce": [float(size)],
+        "scatter": [rank + 1.0],
+        "all_gather": [float(r) for r in range(size)],
+        "broadcast": [0.0],
+    }
+    if rank == 0:
+        e["reduce"] = [float(size)]
+        e["gather"] = [float(r) for r in range(size)]
+    else:
+        # non-root reduce buffers are left untouched (Gloo's 3,2,1 leftovers in
+        # README.md:106-109 are an implementation artifact, not a contract)
+        e["reduce"] = [1.0]
+    return e
+
+
+def op_matrix(rank, size, device="cpu", dtypes=("float32", "float64", "int32", "int64", "bfloat16", "float16")):
+    """all_reduce and reduce for every ReduceOp x dtype with t=[r+2, 10-r, r]
+    (the survey's probe)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    res = {}
+    for dt in dtypes:
+        tdt = getattr(torch, dt)
+        for op in ("SUM", "PRODUCT", "MAX", "MIN", "AVG"):
+            if op == "AVG" and not tdt.is_floating_point:
+                continue
+            t = torch.tensor([rank + 2, 10 - rank, rank], dtype=tdt, device=d)
+            dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+            res[f"all_reduce/{dt}/{op}"] = t.float().cpu().tolist()
+            t = torch.tensor([rank + 2, 10 - rank, rank], dtype=tdt, device=d)
+            dist.reduce(t, dst=size - 1, op=getattr(dist.ReduceOp, op))
+            if rank == size - 1:
+                res[f"reduce/{dt}/{op}"] = t.float().cpu().tolist()
+        if not tdt.is_floating_point:
+            for op in ("BAND", "BOR", "BXOR"):
+                t = torch.tensor([rank + 2, 10 - rank, rank], dtype=tdt, device=d)
+                dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+                res[f"all_reduce/{dt}/{op}"] = t.float().cpu().tolist()
+    return res
+
+
+def expected_op(size, op):
+    import functools
+
+    vals = [[r + 2, 10 - r, r] for r in range(size)]
+    cols = list(zip(*vals))
+    f = {
+        "SUM": sum,
+        "PRODUCT": lambda c: functools.reduce(lambda a, b: a * b, c),
+        "MAX": max,
+        "MIN": min,
+        "AVG": lambda c: sum(c) / len(c),
+        "BAND": lambda c: functools.reduce(lambda a, b: a & b, c),
+        "BOR": lambda c: functools.reduce(lambda a, b: a | b, c),
+        "BXOR": lambda c: functools.reduce(lambda a, b: a ^ b, c),
+    }[op]
+    return [float(f(c)) for c in cols]
+
+
+def large(rank, size, device="cpu", n=3_000_017):
+    """Bulk paths (chunking across shm slots / IPC staging, tails not multiple of 16 B)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ok = {}
+    base = torch.arange(n, dtype=torch.float32, device=d) % 1000
+    t = base * (rank + 1)
+    dist.all_reduce(t)
+    ok["all_reduce"] = bool(torch.equal(t, base * (size * (size + 1) // 2)))
+    t = base * (rank + 1)
+    dist.reduce(t, dst=0)
+    ok["reduce"] = bool(torch.equal(t, base * (size * (size + 1) // 2))) if rank == 0 else bool(torch.equal(t, base * (rank + 1)))
+    t = base.clone() if rank == 0 else torch.zeros_like(base)
+    dist.broadcast(t, src=0)
+    ok["broadcast"] = bool(torch.equal(t, base))
+    m = n // 7 + 3
+    lst = [torch.empty(m, dtype=torch.float32, device=d) for _ in range(size)]
+    dist.all_gather(lst, torch.full((m,), float(rank), device=d))
+    ok["all_gather"] = all(bool(torch.all(x == r)) for r, x in enumerate(lst))
+    o = torch.empty(size * m, device=d)
+    dist.all_gather_into_tensor(o, torch.full((m,), float(rank), device=d))
+    ok["all_gather_into_tensor"] = bool(torch.equal(o, torch.arange(size, device=d).float().repeat_interleave(m)))
+    inp = torch.arange(size * m, dtype=torch.float32, device=d) % 97
+    o = torch.empty(m, device=d)
+    dist.reduce_scatter_tensor(o, inp)
+    ok["reduce_scatter_tensor"] = bool(torch.equal(o, (inp * size)[rank * m:(rank + 1) * m]))
+    ins = [torch.full((m,), float(rank * 100 + q), device=d) for q in range(size)]
+    outs = [torch.empty(m, device=d) for _ in range(size)]
+    dist.all_to_all(outs, ins)
+    ok["all_to_all"] = all(bool(torch.all(outs[q] == q * 100 + rank)) for q in range(size))
+    x = torch.arange(size * 5, dtype=torch.float32, device=d) + 1000 * rank
+    y = torch.empty_like(x)
+    dist.all_to_all_single(y, x)
+    exp = torch.cat([torch.arange(rank * 5, rank * 5 + 5, dtype=torch.float32) + 1000 * q for q in range(size)])
+    ok["all_to_all_single"] = bool(torch.equal(y.cpu(), exp))
+    # uneven splits: rank r sends (q+1) rows to q
+    in_splits = [q + 1 for q in range(size)]
+    out_splits = [rank + 1] * size
+    x = torch.cat([torch.full((q + 1, 3), float(rank * 10 + q)) for q in range(size)]).to(d)
+    y = torch.empty(sum(out_splits), 3, device=d)
+    dist.all_to_all_single(y, x, out_splits, in_splits)
+    exp = torch.cat([torch.full((rank + 1, 3), float(q * 10 + rank)) for q in range(size)])
+    ok["all_to_all_single_uneven"] = bool(torch.equal(y.cpu(), exp))
+    dist.barrier()
+    return ok
+
+
+def noncontig(rank, size, device="cpu"):
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    a = torch.arange(64, dtype=torch.float32, device=d).reshape(8, 8) * (rank + 1)
+    v = a.t()  # non-contiguous view
+    dist.all_reduce(v)
+    s = size * (size + 1) // 2
+    ok1 = bool(torch.equal(a, torch.arange(64, dtype=torch.float32, device=d).reshape(8, 8) * s))
+    b = (torch.arange(20, dtype=torch.float32, device=d) + rank)[1:]  # misaligned view (offset 4 B)
+    dist.all_reduce(b)
+    ok2 = bool(torch.equal(b, (torch.arange(20, dtype=torch.float32, device=d) * size + s - size)[1:]))
+    return {"transposed": ok1, "offset": ok2}
+
+
+def subgroup_evens(rank, size, device="cpu"):
+    import torch
+    import torch.distributed as dist
+
+    evens = list(range(0, size, 2))
+    g = dist.new_group(evens)
+    t = torch.tensor([float(rank)], device=_dev(device))
+    if rank in evens:
+        dist.all_reduce(t, group=g)
+    return t.item()
+
+
+def p2p(rank, size, device="cpu", n=600_000):
+    """Ring exchange with isend/irecv larger than the p2p channel, then a batch."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    x = torch.full((n,), float(rank), device=d)
+    y = torch.empty(n, device=d)
+    s = dist.isend(x, nxt)
+    r = dist.irecv(y, prv)
+    s.wait()
+    r.wait()
+    ok1 = bool(torch.all(y == prv))
+    y2 = torch.empty(n, device=d)
+    ops = [dist.P2POp(dist.isend, x * 2, nxt), dist.P2POp(dist.irecv, y2, prv)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    ok2 = bool(torch.all(y2 == 2 * prv))
+    return {"ring": ok1, "batch": ok2}
+
+
+def errors(rank, size):
+    """Argument errors must raise on every rank (SURVEY.md §4.2 error contracts)."""
+    import torch
+    import torch.distributed as dist
+
+    msgs = {}
+    try:
+        dist.broadcast(torch.ones(1), src=size)
+    except (RuntimeError, ValueError) as e:
+        msgs["bad_root"] = str(e)
+    try:
+        dist.all_gather([torch.empty(1) for _ in range(size + 1)], torch.ones(1))
+    except (RuntimeError, ValueError) as e:
+        msgs["bad_list"] = str(e)
+    # the group is still usable afterwards
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    msgs["after"] = t.item()
+    return msgs
+
+
+def debug_mismatch(rank, size):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.ones(4 + rank)  # per-rank shape mismatch: silent with Gloo on rank 0
+    try:
+        dist.all_reduce(t)
+        return "no error"
+    except RuntimeError as e:
+        return str(e)
+
+
+def stats_probe(rank, size):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend
+
+    t = torch.ones(16)
+    dist.all_reduce(t)
+    st = backend.stats()
+    return {k: list(v) for k, v in st.items()}, backend.describe()
+
+
+def timing_allreduce(rank, size, n=1 << 20, iters=20):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.ones(n)
+    dist.all_reduce(t)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(t)
+    return (time.perf_counter() - t0) / iters
+
+
+def fault_victim(rank, size, q):
+    """rank 1 dies (PDCC_FAULT=1:3:exit); rank 0 must get an error, fast."""
+    import datetime
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import init_process
+
+    def body(r, s):
+        t0 = time.time()
+        try:
+            for _ in range(50):
+                x = torch.ones(8)
+                dist.all_reduce(x)
+            return ("no error", time.time() - t0)
+        except RuntimeError as e:
+            return (str(e), time.time() - t0)
+
+    res = init_process(rank, size, body, timeout_s=60)
+    q.put((rank, res))

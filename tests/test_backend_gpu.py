@@ -1,0 +1,78 @@
+"""The mi355x backend on GPU tensors (1 MI355X box).
+
+* world of 1: local fast path, and RCCL forced on a 1-rank communicator
+  (PDCC_WORLD1_LOCAL=0) so every RCCL call site and dtype/op mapping runs;
+* several processes sharing cuda:0: RCCL refuses duplicate devices, so these
+  runs exercise the hipIpc peer-memory path (our K1/K3/K4 kernels, 1-shot and
+  2-shot protocols, chunking, parity double-buffering) and the host-staged
+  fallback, with the reference's golden outputs as the oracle.
+"""
+import pytest
+import torch
+
+from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+from tests import _workers as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_launch(fn, world, args=("cuda",), env=None, timeout_s=60):
+    e = {"PDCC_IPC_TIMEOUT_HINT": "1"}
+    e.update(env or {})
+    return launch(fn, world, args=args, bind_device=True, timeout_s=timeout_s, env=e, join_timeout_s=600)
+
+
+@pytest.mark.parametrize("world1_local", ["1", "0"])
+def test_world1_golden(world1_local):
+    res = _gpu_launch(W.golden, 1, env={"PDCC_WORLD1_LOCAL": world1_local})
+    assert res[0] == W.expected_golden(0, 1)
+
+
+def test_world1_rccl_bulk_paths():
+    res = _gpu_launch(W.large, 1, env={"PDCC_WORLD1_LOCAL": "0"})
+    assert all(res[0].values()), res[0]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_shared_gpu_ipc_golden(world):
+    res = _gpu_launch(W.golden, world, env={"PDCC_ALGO": "ipc"})
+    for r, got in enumerate(res):
+        assert got == W.expected_golden(r, world), (r, got)
+
+
+def test_shared_gpu_ipc_op_matrix():
+    world = 3
+    res = _gpu_launch(W.op_matrix, world, args=("cuda", ("float32", "int32", "bfloat16", "int64")),
+                      env={"PDCC_ALGO": "ipc"})
+    for got in res:
+        for key, val in got.items():
+            kind, dt, op = key.split("/")
+            exp = W.expected_op(world, op)
+            if dt == "bfloat16":
+                assert val == pytest.approx(exp, rel=1e-2), key
+            else:
+                assert val == pytest.approx(exp), key
+
+
+@pytest.mark.parametrize("oneshot_max", ["512K", "0"])
+def test_shared_gpu_ipc_bulk(oneshot_max):
+    # small staging forces the chunked path; 1SHOT_MAX=0 forces 2-shot everywhere
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": oneshot_max, "PDCC_IPC_MAX_STAGING": "2M"}
+    for ok in _gpu_launch(W.large, 2, env=env):
+        assert all(ok.values()), ok
+
+
+def test_shared_gpu_noncontig():
+    for ok in _gpu_launch(W.noncontig, 2, env={"PDCC_ALGO": "ipc"}):
+        assert all(ok.values()), ok
+
+
+def test_shared_gpu_host_fallback():
+    res = _gpu_launch(W.golden, 2, env={"PDCC_ALGO": "host"})
+    for r, got in enumerate(res):
+        assert got == W.expected_golden(r, 2), (r, got)
+
+
+def test_shared_gpu_p2p_host_staged():
+    for ok in _gpu_launch(W.p2p, 2, args=("cuda", 1000)):
+        assert all(ok.values()), ok

@@ -1,0 +1,105 @@
+"""Multi-process CPU tests of the mi355x backend (shared-memory host transport).
+
+The reference's only "test" is running main.py and reading stdout (SURVEY.md
+§4.1); these tests check the same golden outputs automatically, for every
+world size the survey probed (1/2/4/8), plus ops x dtypes, bulk paths,
+sub-groups, p2p, argument errors, the PDCC_DEBUG fingerprint check and fault
+detection.
+"""
+import os
+
+import pytest
+
+from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+from tests import _workers as W
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_golden_outputs(world):
+    res = launch(W.golden, world, args=("cpu",))
+    for r, got in enumerate(res):
+        assert got == W.expected_golden(r, world), (r, got)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_op_matrix(world):
+    res = launch(W.op_matrix, world, args=("cpu",))
+    for r, got in enumerate(res):
+        for key, val in got.items():
+            kind, dt, op = key.split("/")
+            exp = W.expected_op(world, op)
+            if dt in ("int32", "int64") and op == "AVG":
+                continue
+            if dt in ("bfloat16", "float16"):
+                assert val == pytest.approx(exp, rel=1e-2), key
+            else:
+                assert val == pytest.approx(exp), key
+        if r == world - 1:
+            assert any(k.startswith("reduce/") for k in got)
+
+
+@pytest.mark.parametrize("world", [1, 3, 4])
+def test_large_and_uneven(world):
+    for r, ok in enumerate(launch(W.large, world, args=("cpu",))):
+        assert all(ok.values()), (r, ok)
+
+
+def test_noncontiguous_and_offset_views():
+    for ok in launch(W.noncontig, 2, args=("cpu",)):
+        assert all(ok.values()), ok
+
+
+def test_subgroup_evens():
+    res = launch(W.subgroup_evens, 4, args=("cpu",))
+    assert res == [2.0, 1.0, 2.0, 3.0]
+
+
+def test_p2p_ring_and_batch():
+    for ok in launch(W.p2p, 3, args=("cpu",)):
+        assert all(ok.values()), ok
+
+
+def test_argument_errors_raise_everywhere():
+    for m in launch(W.errors, 2):
+        assert "invalid root rank" in m["bad_root"]
+        assert "expected length 2, got 3" in m["bad_list"]
+        assert m["after"] == 2.0
+
+
+def test_debug_fingerprint_catches_shape_mismatch():
+    res = launch(W.debug_mismatch, 2, env={"PDCC_DEBUG": "1"})
+    for msg in res:
+        assert "collective mismatch" in msg, msg
+
+
+def test_stats_and_describe():
+    res = launch(W.stats_probe, 2)
+    st, desc = res[0]
+    assert st["allreduce/shm"][0] >= 1
+    assert "ProcessGroupMI355X" in desc and "size=2" in desc
+
+
+def test_peer_death_is_detected_quickly():
+    import torch.multiprocessing as mp
+
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    os.environ["MASTER_PORT"] = str(free_port())
+    os.environ["PDCC_FAULT"] = "1:5:exit"
+    try:
+        ps = [ctx.Process(target=W.fault_victim, args=(r, 2, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        rank, (msg, elapsed) = q.get(timeout=120)
+    finally:
+        os.environ.pop("PDCC_FAULT", None)
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert rank == 0
+    assert "exited" in msg or "aborted" in msg, msg
+    assert elapsed < 20, elapsed
+    assert ps[1].exitcode == 13
