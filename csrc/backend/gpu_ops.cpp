@@ -10,8 +10,8 @@
 //           grouped ncclSend/Recv (gather/scatter/uneven all-to-all/p2p)
 //   HOST -- D2H, the shared-memory host transport, H2D (fallback only)
 #include <ATen/hip/HIPContext.h>
-#include <c10/hip/HIPCachingAllocator.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <unistd.h>
 
@@ -130,7 +130,7 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   if (it != devs_.end()) return *it->second;
   TORCH_CHECK(devs_.empty(), "pdcc: one GPU per rank per process group (got a tensor on cuda:", d,
               " after using cuda:", devs_.begin()->first, ")");
-  c10::hip::HIPGuard g((c10::DeviceIndex)d);
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)d);
   char bus[64] = {0};
   PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
   char host[256] = {0};
@@ -159,7 +159,7 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
   for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
 
-  auto ds = std::make_unique<DeviceState>(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)d));
+  auto ds = std::make_unique<DeviceState>(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true, (c10::DeviceIndex)d));
   ds->device = d;
   ds->shared_device = shared;
   ds->rccl_ok = !shared;
@@ -231,8 +231,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
                                                            std::chrono::milliseconds timeout,
                                                            const std::function<void(hipStream_t)>& fn,
                                                            std::shared_ptr<IpcComm> ipcp) {
-  c10::hip::HIPGuard g((c10::DeviceIndex)ds.device);
-  auto cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)ds.device);
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
+  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
   hipEvent_t pre = ds.get_event();
   PDCC_HIP(hipEventRecord(pre, cur.stream()));
   PDCC_HIP(hipStreamWaitEvent(ds.stream.stream(), pre, 0));
@@ -240,14 +240,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   const bool rx = cfg_.roctx && roctx_push_;
   if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
   {
-    c10::hip::HIPStreamGuard sg(ds.stream);  // temporaries + copy-backs run on the comm stream
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);  // temporaries + copy-backs run on the comm stream
     fn(ds.stream.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
   for (const auto& t : keep_alive)
-    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), ds.stream);
+    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), ds.stream);
   for (const auto& t : outputs)
-    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), ds.stream);
+    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), ds.stream);
   hipEvent_t ev;
   PDCC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   PDCC_HIP(hipEventRecord(ev, ds.stream.stream()));

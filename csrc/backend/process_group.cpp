@@ -4,8 +4,8 @@
 #include "process_group.h"
 
 #include <ATen/hip/HIPContext.h>
-#include <c10/hip/HIPCachingAllocator.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <dlfcn.h>
 #include <unistd.h>
 
@@ -37,7 +37,7 @@ WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at
 }
 
 WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs, c10::Device dev,
-                       hipEvent_t ev, c10::hip::HIPStream comm, std::shared_ptr<Health> health, bool blocking,
+                       hipEvent_t ev, c10::hip::HIPStreamMasqueradingAsCUDA comm, std::shared_ptr<Health> health, bool blocking,
                        std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc)
     : c10d::Work(rank, type),
       seq_(seq),
@@ -52,7 +52,7 @@ WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at
       start_(std::chrono::steady_clock::now()) {
   std::vector<c10::Device> devs{dev_};
   fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
-  c10::hip::HIPStreamGuard g(comm);  // the future's events are recorded on the comm stream
+  c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm);  // the future's events are recorded on the comm stream
   fut_->markCompleted(c10::IValue(outputs_));
 }
 
@@ -101,8 +101,8 @@ bool WorkMI355X::isSuccess() const {
 
 void WorkMI355X::synchronize() {
   if (!gpu_) return;
-  c10::hip::HIPGuard g(dev_);
-  auto cur = c10::hip::getCurrentHIPStream(dev_.index());
+  c10::hip::HIPGuardMasqueradingAsCUDA g(dev_);
+  auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev_.index());
   PDCC_HIP(hipStreamWaitEvent(cur.stream(), ev_, 0));
 }
 

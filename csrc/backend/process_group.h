@@ -14,7 +14,7 @@
 //                   HOST : D2H + shm + H2D (only when neither of the above can)
 #pragma once
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/csrc/distributed/c10d/Backend.hpp>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 #include <torch/csrc/distributed/c10d/Work.hpp>
@@ -64,7 +64,7 @@ class WorkMI355X : public c10d::Work {
   WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs);
   // GPU work: `ev` recorded on the comm stream after the enqueued collective
   WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs, c10::Device dev,
-             hipEvent_t ev, c10::hip::HIPStream comm, std::shared_ptr<Health> health, bool blocking,
+             hipEvent_t ev, c10::hip::HIPStreamMasqueradingAsCUDA comm, std::shared_ptr<Health> health, bool blocking,
              std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc);
   ~WorkMI355X() override;
 
@@ -100,7 +100,7 @@ class WorkMI355X : public c10d::Work {
 
 struct DeviceState {
   int device = -1;
-  c10::hip::HIPStream stream;           // high-priority comm stream
+  c10::hip::HIPStreamMasqueradingAsCUDA stream;           // high-priority comm stream
   bool rccl_ok = false;                 // all ranks on distinct devices
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
   bool shared_device = false;           // several ranks share one GPU (test setups)
@@ -108,7 +108,7 @@ struct DeviceState {
   std::shared_ptr<IpcComm> ipc;         // lazy
   std::mutex ev_mu;
   std::vector<hipEvent_t> ev_pool;
-  explicit DeviceState(c10::hip::HIPStream s) : stream(s) {}
+  explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
   hipEvent_t get_event();
   void put_event(hipEvent_t e);
 };

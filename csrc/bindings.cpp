@@ -3,7 +3,7 @@
 //  * kernel ops           -- K1 reduce_nway (LDS-DMA and register variants) and
 //                            K2 multi_copy on torch tensors, on the current stream
 #include <ATen/hip/HIPContext.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <pybind11/chrono.h>
 #include <pybind11/stl.h>
 #include <torch/csrc/utils/pybind.h>
@@ -61,8 +61,8 @@ void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std
   const auto k = kop(op);
   const auto d = kdtype(out.scalar_type());
   TORCH_CHECK(pdcc::kern::supports(d, k), "reduce_nway: op '", op, "' unsupported for ", out.scalar_type());
-  c10::hip::HIPGuard g(out.device());
-  hipStream_t s = c10::hip::getCurrentHIPStream(out.device().index()).stream();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(out.device().index()).stream();
   hipError_t e = lds ? pdcc::kern::reduce_nway(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
                                                (int)srcs.size(), s, max_blocks)
                      : pdcc::kern::reduce_nway_regs(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
@@ -79,12 +79,11 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
     const auto& b = dsts[i];
     TORCH_CHECK(a.is_cuda() && b.device() == a.device(), "multi_copy: tensors must be on one GPU");
     TORCH_CHECK(a.nbytes() == b.nbytes(), "multi_copy: pair ", i, " size mismatch");
-    TORCH_CHECK(a.is_contiguous() && b.is_contiguous() && al16(a.data_ptr()) && al16(b.data_ptr()),
-                "multi_copy: tensors must be contiguous and 16-byte aligned");
+    TORCH_CHECK(a.is_contiguous() && b.is_contiguous(), "multi_copy: tensors must be contiguous");
     d.push_back({a.data_ptr(), b.data_ptr(), a.nbytes()});
   }
-  c10::hip::HIPGuard g(srcs[0].device());
-  hipStream_t s = c10::hip::getCurrentHIPStream(srcs[0].device().index()).stream();
+  c10::hip::HIPGuardMasqueradingAsCUDA g(srcs[0].device());
+  hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(srcs[0].device().index()).stream();
   hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s);
   TORCH_CHECK(e == hipSuccess, "multi_copy launch failed: ", hipGetErrorString(e));
 }

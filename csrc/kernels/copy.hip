@@ -193,6 +193,7 @@ hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t
 }
 
 hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream) {
+  auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   for (int base = 0; base < n; base += kMaxCopyDescs) {
     dev::CopyArgs a{};
     const int m = std::min(kMaxCopyDescs, n - base);
@@ -201,6 +202,12 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream) {
     for (int k = 0; k < m; ++k) {
       a.d[a.n] = descs[base + k];
       if (a.d[a.n].bytes == 0) continue;
+      if (!aligned(a.d[a.n].src) || !aligned(a.d[a.n].dst)) {
+        // the 16-B vector / LDS-DMA path needs aligned endpoints: DMA engine copy instead
+        hipError_t e = hipMemcpyAsync(a.d[a.n].dst, a.d[a.n].src, a.d[a.n].bytes, hipMemcpyDeviceToDevice, stream);
+        if (e != hipSuccess) return e;
+        continue;
+      }
       a.prefix[a.n] = acc;
       acc += a.d[a.n].bytes / kTileBytes;
       if (a.d[a.n].bytes % kTileBytes) a.tail_idx[a.ntail++] = a.n;

@@ -177,6 +177,7 @@ struct PipeLds {
 template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   static_assert((DEPTH - 1) * (NSRC + 1) < 64, "pipeline too deep for vmcnt");
+  static_assert(DEPTH >= 2 && DEPTH <= 4, "prologue wait counts are written out for DEPTH <= 4");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const uint32_t lane_off = wave * kWaveBytes + lane * 16;
@@ -224,9 +225,20 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
     int ns = stage + DEPTH - 1;
     if (ns >= DEPTH) ns -= DEPTH;
     issue(i + DEPTH - 1, ns);
-    // outstanding after tile i's loads: (DEPTH-1) younger tiles x NSRC loads
-    // plus one store per consumed tile in between
-    wait_vmcnt<(DEPTH - 1) * (NSRC + 1)>();
+    // Ops younger than tile i's loads: the (DEPTH-1) tiles issued after it
+    // (x NSRC loads) plus the stores of the consumes in between -- i of them
+    // while tile i was a prologue tile, DEPTH-1 in steady state. vmcnt retires
+    // in issue order, so the count must be exact (a looser one lets tile i's
+    // last load still be in flight when its LDS slot is read).
+    if (i >= (size_t)(DEPTH - 1)) {
+      wait_vmcnt<(DEPTH - 1) * (NSRC + 1)>();
+    } else if (i == 0) {
+      wait_vmcnt<(DEPTH - 1) * NSRC>();
+    } else if (i == 1) {
+      wait_vmcnt<(DEPTH - 1) * NSRC + (DEPTH > 2 ? 1 : 0)>();
+    } else {
+      wait_vmcnt<(DEPTH - 1) * NSRC + (DEPTH > 3 ? 2 : 0)>();
+    }
     consume(i, stage);
     stage = (stage + 1 == DEPTH) ? 0 : stage + 1;
   }

@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU validation run for gpurun: each GPU step under its own time limit; a test
+# FAILURE (pytest rc 1) does not stop the chain, a crash/timeout/abort does.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    smoke) step smoke 300 python __graft_entry__.py ;;
+    kern) step kern 600 python -m pytest tests/test_kernels_gpu.py -x -q ;;
+    backend) step backend 900 python -m pytest tests/test_backend_gpu.py -x -q ;;
+    gputests) step gputests 1200 python -m pytest tests -m gpu -q ;;
+    bench1) step bench1 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    kprof) step kprof 600 python scripts/kernel_bench.py ;;
+  esac
+done
