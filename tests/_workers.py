@@ -293,3 +293,56 @@ def fault_victim(rank, size, q):
 
     res = init_process(rank, size, body, timeout_s=60)
     q.put((rank, res))
+
+
+def demo(rank, size, name, device="cpu"):
+    from pytorch_distributed_collective_communication_amd.models.demos import DEMOS
+
+    return DEMOS[name](rank, size, device)
+
+
+def dp_train(rank, size, mode="bucketer", steps=5, device="cpu", bucket_bytes=2048):
+    """Data-parallel SGD on the MLP; returns the flattened final parameters."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.models import MLP, synthetic_batch
+    from pytorch_distributed_collective_communication_amd.parallel import ddp
+
+    d = _dev(device)
+    torch.manual_seed(100 + rank)  # deliberately different init: broadcast must fix it
+    model = MLP().to(d)
+    ddp.broadcast_parameters(model, src=0)
+    x, y = synthetic_batch(64, device=d)
+    shard = 64 // size
+    xs, ys = x[rank * shard:(rank + 1) * shard], y[rank * shard:(rank + 1) * shard]
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    if mode == "torch_ddp":
+        net = torch.nn.parallel.DistributedDataParallel(model)
+    else:
+        net = model
+        buck = ddp.GradBucketer(model, bucket_bytes=bucket_bytes)
+    for _ in range(steps):
+        opt.zero_grad(set_to_none=False)
+        loss = torch.nn.functional.mse_loss(net(xs), ys)
+        loss.backward()
+        if mode != "torch_ddp":
+            buck.finish()
+        opt.step()
+    return torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+
+
+def dp_reference(steps=5):
+    import torch
+
+    from pytorch_distributed_collective_communication_amd.models import MLP, synthetic_batch
+
+    torch.manual_seed(100)
+    model = MLP()
+    x, y = synthetic_batch(64)
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    for _ in range(steps):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
