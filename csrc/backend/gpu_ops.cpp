@@ -271,6 +271,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.emplace_back(w);
   }
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    fr_last_work_ = w;  // picked up by record() for the flight recorder
+  }
   return w;
 }
 

@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <sstream>
 
@@ -285,6 +286,7 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
     roctx_push_ = roctx().push;
     roctx_pop_ = roctx().pop;
   }
+  if (const char* fr = std::getenv("PDCC_FLIGHT_RECORDER")) fr_cap_ = (size_t)std::max(0, std::atoi(fr));
   if (cfg_.watchdog_ms > 0) wd_thr_ = std::thread([this] { watchdog_loop(); });
 }
 
@@ -378,11 +380,48 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
 void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0) {
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> lk(stats_mu_);
-  OpStats& s = stats_[std::string(coll_name(c)) + "/" + algo];
+  const std::string key = std::string(coll_name(c)) + "/" + algo;
+  OpStats& s = stats_[key];
   s.calls++;
   s.bytes += bytes;
   s.host_ms += ms;
   last_algo_ = algo;
+  if (fr_cap_ > 0) {
+    FrEntry e{op_seq_.load(), key, bytes,
+              std::chrono::duration<double, std::milli>(t0 - created_).count(), (bool)fr_last_work_,
+              fr_last_work_ ? c10::weak_intrusive_ptr<WorkMI355X>(fr_last_work_)
+                            : c10::weak_intrusive_ptr<WorkMI355X>(c10::intrusive_ptr<WorkMI355X>())};
+    fr_last_work_.reset();
+    fr_.push_back(std::move(e));
+    while (fr_.size() > fr_cap_) fr_.pop_front();
+  }
+}
+
+std::vector<ProcessGroupMI355X::FrRecord> ProcessGroupMI355X::flight_recorder() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  std::vector<FrRecord> out;
+  for (auto& e : fr_) {
+    std::string st = "done";
+    if (e.gpu) {
+      auto w = e.work.lock();
+      if (!w) st = "released";
+      else if (!w->isCompleted()) st = "pending";
+      else if (!w->isSuccess()) st = "failed";
+    }
+    out.push_back({e.seq, e.what, e.bytes, e.t_ms, st});
+  }
+  return out;
+}
+
+std::string ProcessGroupMI355X::flight_recorder_dump(size_t last) {
+  auto recs = flight_recorder();
+  std::ostringstream o;
+  o << "[pdcc] flight recorder, rank " << rank_ << ", last " << std::min(last, recs.size()) << " of " << recs.size()
+    << " ops:\n";
+  for (size_t i = recs.size() > last ? recs.size() - last : 0; i < recs.size(); ++i)
+    o << "  #" << recs[i].seq << " " << recs[i].what << " bytes=" << recs[i].bytes << " t=" << recs[i].t_ms
+      << "ms state=" << recs[i].state << "\n";
+  return o.str();
 }
 
 std::map<std::string, OpStats> ProcessGroupMI355X::stats() {
@@ -459,7 +498,7 @@ void ProcessGroupMI355X::watchdog_loop() {
         const std::string msg = "watchdog: collective #" + std::to_string(w->getSequencenumber()) + " on rank " +
                                 std::to_string(rank_) + " exceeded its timeout of " +
                                 std::to_string(w->timeout().count()) + " ms; aborting the group";
-        fprintf(stderr, "[pdcc] %s\n", msg.c_str());
+        fprintf(stderr, "[pdcc] %s\n%s", msg.c_str(), flight_recorder_dump().c_str());
         w->fail(msg);
         abort_group(msg);
         continue;

@@ -266,6 +266,32 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::vector<at::Tensor> coalesced_tensors_;
   DeviceState* coalesced_ds_ = nullptr;
 
+  // flight recorder: the last N collectives (seq, what, bytes, enqueue time, work)
+  struct FrEntry {
+    uint64_t seq;
+    std::string what;
+    size_t bytes;
+    double t_ms;
+    bool gpu;
+    c10::weak_intrusive_ptr<WorkMI355X> work;
+  };
+  std::deque<FrEntry> fr_;
+  size_t fr_cap_ = 256;
+  c10::intrusive_ptr<WorkMI355X> fr_last_work_;
+  std::chrono::steady_clock::time_point created_ = std::chrono::steady_clock::now();
+
+ public:
+  struct FrRecord {
+    uint64_t seq;
+    std::string what;
+    uint64_t bytes;
+    double t_ms;
+    std::string state;
+  };
+  std::vector<FrRecord> flight_recorder();
+  std::string flight_recorder_dump(size_t last = 16);
+
+ private:
   std::vector<c10::intrusive_ptr<WorkMI355X>> coalesced_cpu_;
   int (*roctx_push_)(const char*) = nullptr;
   int (*roctx_pop_)() = nullptr;

@@ -111,6 +111,21 @@ PYBIND11_MODULE(_C, m) {
                d[py::str(kv.first)] = py::make_tuple(kv.second.calls, kv.second.bytes, kv.second.host_ms);
              return d;
            })
+      .def("flight_recorder",
+           [](pdcc::ProcessGroupMI355X& pg) {
+             py::list l;
+             for (const auto& r : pg.flight_recorder()) {
+               py::dict d;
+               d["seq"] = r.seq;
+               d["op"] = r.what;
+               d["bytes"] = r.bytes;
+               d["t_ms"] = r.t_ms;
+               d["state"] = r.state;
+               l.append(d);
+             }
+             return l;
+           })
+      .def("flight_recorder_dump", &pdcc::ProcessGroupMI355X::flight_recorder_dump, py::arg("last") = 16)
       .def("reset_stats", &pdcc::ProcessGroupMI355X::reset_stats)
       .def("describe", &pdcc::ProcessGroupMI355X::describe)
       .def("last_algo", &pdcc::ProcessGroupMI355X::last_algo)

@@ -1,0 +1,106 @@
+"""Python mirror of the backend's PDCC_* configuration (csrc/backend/config.h).
+
+The native backend reads these environment variables once, when a process
+group is constructed; :func:`current` shows what a new group would use and
+:func:`env_for` builds an environment dict (e.g. for ``parallel.spawn.launch``).
+
+| variable | default | meaning |
+|---|---|---|
+| PDCC_ALGO | auto | force ``rccl`` / ``ipc`` / ``host`` for GPU tensors (preferred if feasible) |
+| PDCC_IPC | 1 | enable the hipIpc peer-memory path |
+| PDCC_IPC_1SHOT_MAX | 512K | all-reduce/reduce/broadcast up to this size: 1-shot protocol |
+| PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
+| PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
+| PDCC_IPC_MAX_STAGING | 512M | staging bytes per parity; larger calls are chunked |
+| PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
+| PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
+| PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
+| PDCC_DEBUG | 0 | cross-rank fingerprint check before every collective |
+| PDCC_LOG_LEVEL | 0 | 1: group/device info, 2: every collective |
+| PDCC_BLOCKING_WAIT | 0 | ``Work.wait()`` blocks the host until the GPU op finished |
+| PDCC_ROCTX | 0 | roctx range per collective (rocprofv3 --marker-trace) |
+| PDCC_WATCHDOG_MS | 100 | watchdog poll period (0 disables timeout/abort handling) |
+| PDCC_FLIGHT_RECORDER | 256 | number of recent collectives kept for post-mortem dumps |
+| PDCC_FAULT | "" | fault injection ``rank:op_seq:kind`` (kind exit, raise, hang) |
+| PDCC_TAKEOVER_GLOO / _NCCL | 0 | serve ``init_process_group("gloo"/"nccl")`` with mi355x |
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, fields
+
+_SUFFIX = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+
+
+def parse_bytes(v: str | int) -> int:
+    if isinstance(v, int):
+        return v
+    v = v.strip()
+    for suf in ("KiB", "MiB", "GiB"):
+        if v.endswith(suf):
+            v = v[:-3] + suf[0]
+    if v and v[-1].upper() in _SUFFIX:
+        return int(float(v[:-1]) * _SUFFIX[v[-1].upper()])
+    return int(float(v))
+
+
+@dataclass
+class Config:
+    algo: str = "auto"
+    ipc: bool = True
+    ipc_1shot_max: int = 512 << 10
+    ipc_2shot_max: int = 8 << 20
+    ipc_copy_max: int = 1 << 20
+    ipc_max_staging: int = 512 << 20
+    world1_local: bool = True
+    shm_slot_bytes: int = 8 << 20
+    shm_chan_bytes: int = 1 << 20
+    debug: bool = False
+    log_level: int = 0
+    blocking_wait: bool = False
+    roctx: bool = False
+    watchdog_ms: int = 100
+    flight_recorder: int = 256
+    fault: str = ""
+
+
+_ENV = {
+    "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
+    "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "world1_local": "PDCC_WORLD1_LOCAL",
+    "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES", "debug": "PDCC_DEBUG",
+    "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",
+    "watchdog_ms": "PDCC_WATCHDOG_MS", "flight_recorder": "PDCC_FLIGHT_RECORDER", "fault": "PDCC_FAULT",
+}
+
+
+def _parse(field_type, raw: str):
+    if field_type in (bool, "bool"):
+        return raw.strip().lower() not in ("0", "false", "no", "off", "")
+    if field_type in (int, "int"):
+        return parse_bytes(raw)
+    return raw
+
+
+def current(environ=None) -> Config:
+    """The configuration a process group created now would get."""
+    env = os.environ if environ is None else environ
+    c = Config()
+    for f in fields(Config):
+        raw = env.get(_ENV[f.name])
+        if raw not in (None, ""):
+            setattr(c, f.name, _parse(f.type, raw))
+    if c.algo not in ("auto", "rccl", "ipc", "host"):
+        raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|host, got {c.algo!r}")
+    return c
+
+
+def env_for(**overrides) -> dict:
+    """Environment entries for the given overrides, e.g. ``env_for(algo="ipc", debug=True)``."""
+    out = {}
+    names = {f.name for f in fields(Config)}
+    for k, v in overrides.items():
+        if k not in names:
+            raise KeyError(f"unknown PDCC config field {k!r}")
+        out[_ENV[k]] = ("1" if v else "0") if isinstance(v, bool) else str(v)
+    return out

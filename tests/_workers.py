@@ -346,3 +346,16 @@ def dp_reference(steps=5):
         torch.nn.functional.mse_loss(model(x), y).backward()
         opt.step()
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+def flight_probe(rank, size):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend
+
+    for n in (1, 10, 100):
+        dist.all_reduce(torch.ones(n))
+    dist.broadcast(torch.ones(3), 0)
+    b = backend.native_backend()
+    return b.flight_recorder(), b.flight_recorder_dump(3)

@@ -76,3 +76,20 @@ def test_shared_gpu_host_fallback():
 def test_shared_gpu_p2p_host_staged():
     for ok in _gpu_launch(W.p2p, 2, args=("cuda", 1000)):
         assert all(ok.values()), ok
+
+
+@pytest.mark.parametrize("name", ["reduce", "all_reduce", "scatter", "gather", "all_gather", "broadcast"])
+def test_tutorial_demos_on_shared_gpu(name):
+    from pytorch_distributed_collective_communication_amd.models.demos import golden
+
+    res = _gpu_launch(W.demo, 2, args=(name, "cuda"))
+    assert res == [golden(name, r, 2) for r in range(2)]
+
+
+@pytest.mark.parametrize("mode", ["bucketer", "torch_ddp"])
+def test_data_parallel_on_shared_gpu(mode):
+    res = _gpu_launch(W.dp_train, 2, args=(mode, 5, "cuda", 1 << 20))
+    ref = W.dp_reference()
+    for p in res:
+        torch.testing.assert_close(p, res[0], rtol=0, atol=0)
+        torch.testing.assert_close(p, ref, rtol=1e-4, atol=1e-5)

@@ -1,0 +1,79 @@
+"""Single-process unit tests: config mirror, busbw math, kernel references,
+package wiring (no GPU, no subprocesses except where noted)."""
+import pytest
+import torch
+
+from pytorch_distributed_collective_communication_amd import config, ops, utils
+from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+from tests import _workers as W
+
+
+def test_parse_bytes():
+    assert config.parse_bytes("512K") == 512 << 10
+    assert config.parse_bytes("8M") == 8 << 20
+    assert config.parse_bytes("1GiB") == 1 << 30
+    assert config.parse_bytes("4096") == 4096
+
+
+def test_config_current_and_env_for():
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_2SHOT_MAX": "16M", "PDCC_DEBUG": "1", "PDCC_IPC": "0"}
+    c = config.current(env)
+    assert c.algo == "ipc" and c.ipc_2shot_max == 16 << 20 and c.debug and not c.ipc
+    assert config.env_for(algo="rccl", debug=True) == {"PDCC_ALGO": "rccl", "PDCC_DEBUG": "1"}
+    with pytest.raises(ValueError):
+        config.current({"PDCC_ALGO": "bogus"})
+    with pytest.raises(KeyError):
+        config.env_for(nope=1)
+
+
+def test_busbw_conventions():
+    assert utils.busbw_factor("all_reduce", 8) == pytest.approx(1.75)
+    assert utils.busbw_factor("broadcast", 8) == 1.0
+    assert utils.busbw_factor("all_gather", 4) == pytest.approx(0.75)
+    assert utils.busbw_factor("all_reduce", 1) == 0.0
+    assert utils.busbw("all_reduce", 1 << 30, 2, 1.0) == pytest.approx((1 << 30) / 1e9)
+    assert utils.xgmi_ceiling_GBps(8) == pytest.approx(7 * 153.0)
+    assert utils.xgmi_ceiling_GBps(2) == pytest.approx(153.0)
+
+
+@pytest.mark.parametrize("op", ["sum", "prod", "min", "max", "avg"])
+def test_reduce_reference_float(op):
+    xs = [torch.tensor([1.0, -2.0, 3.5]), torch.tensor([2.0, 4.0, -1.0]), torch.tensor([0.5, 1.0, 2.0])]
+    got = ops.reduce_nway_reference(xs, op)
+    exp = {"sum": xs[0] + xs[1] + xs[2], "prod": xs[0] * xs[1] * xs[2],
+           "min": torch.minimum(torch.minimum(xs[0], xs[1]), xs[2]),
+           "max": torch.maximum(torch.maximum(xs[0], xs[1]), xs[2]), "avg": (xs[0] + xs[1] + xs[2]) / 3}[op]
+    torch.testing.assert_close(got, exp)
+
+
+def test_reduce_reference_int_and_bool():
+    a, b = torch.tensor([6, 3, -7]), torch.tensor([3, 5, 2])
+    assert torch.equal(ops.reduce_nway_reference([a, b], "band"), a & b)
+    assert torch.equal(ops.reduce_nway_reference([a, b], "bxor"), a ^ b)
+    assert torch.equal(ops.reduce_nway_reference([a, b], "avg"), torch.tensor([4, 4, -2]))
+    t, f = torch.tensor([True, False]), torch.tensor([True, True])
+    assert torch.equal(ops.reduce_nway_reference([t, f], "sum"), t | f)
+
+
+def test_native_extension_loads_and_registers():
+    import torch.distributed as dist
+
+    import pytorch_distributed_collective_communication_amd as pdcc
+
+    C = pdcc._load_native()
+    assert issubclass(C.ProcessGroupMI355X, torch._C._distributed_c10d.Backend)
+    assert "MI355X" in dist.Backend._plugins
+    assert C.TILE_BYTES == 4096 and C.MAX_RANKS_IPC == 8
+
+
+def test_ops_reject_cpu_tensors():
+    with pytest.raises(RuntimeError):
+        ops.reduce_nway([torch.ones(4), torch.ones(4)])
+
+
+def test_flight_recorder():
+    recs, dump = launch(W.flight_probe, 2)[0]
+    ops_ = [r["op"] for r in recs]
+    assert ops_[-4:] == ["allreduce/shm"] * 3 + ["broadcast/shm"]
+    assert all(r["state"] == "done" for r in recs)
+    assert "flight recorder" in dump and "broadcast/shm" in dump
