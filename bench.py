@@ -95,7 +95,8 @@ def main():
     dist.barrier()
     torch.cuda.synchronize()
     total = max_over_ranks(time.perf_counter() - t0)
-    algo = native.last_algo()
+    ar = {k: v[0] for k, v in native.stats().items() if k.startswith("allreduce/")}
+    algo = max(ar, key=ar.get).split("/", 1)[1] if ar else "?"
     ms_per_step = total / args.steps * 1e3
 
     # ---- p50 of individually bracketed steps (BASELINE.md method)
