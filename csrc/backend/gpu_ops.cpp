@@ -233,10 +233,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
                                                            std::shared_ptr<IpcComm> ipcp) {
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
-  hipEvent_t pre = ds.get_event();
+  hipEvent_t pre = ds.events->get();
   PDCC_HIP(hipEventRecord(pre, cur.stream()));
   PDCC_HIP(hipStreamWaitEvent(ds.stream.stream(), pre, 0));
-  ds.put_event(pre);
+  ds.events->put(pre);
   const bool rx = cfg_.roctx && roctx_push_;
   if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
   {
@@ -249,7 +249,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   for (const auto& t : outputs)
     if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), ds.stream);
   hipEvent_t ev;
-  PDCC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  ev = ds.events->get();
   PDCC_HIP(hipEventRecord(ev, ds.stream.stream()));
   auto w = c10::make_intrusive<WorkMI355X>(rank_, [c] {
     switch (c) {
@@ -266,7 +266,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
       default: return c10d::OpType::BARRIER;
     }
   }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, ds.stream,
-                                           health_, cfg_.blocking_wait, timeout, std::move(ipcp));
+                                           health_, cfg_.blocking_wait, timeout, std::move(ipcp), ds.events);
   if (cfg_.watchdog_ms > 0) {
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.emplace_back(w);

@@ -22,24 +22,17 @@ namespace pdcc {
 WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs,
                        std::exception_ptr err)
     : c10d::Work(rank, type), seq_(seq), outputs_(std::move(outputs)), start_(std::chrono::steady_clock::now()) {
-  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()));
-  if (err) {
-    fut_->setError(err);
-    finish(err);
-  } else {
-    fut_->markCompleted(c10::IValue(outputs_));
-    finish();
-  }
+  if (err) finish(err);
+  else finish();
 }
 
 WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs)
-    : c10d::Work(rank, type), seq_(seq), outputs_(std::move(outputs)), start_(std::chrono::steady_clock::now()) {
-  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()));
-}
+    : c10d::Work(rank, type), seq_(seq), outputs_(std::move(outputs)), start_(std::chrono::steady_clock::now()) {}
 
 WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs, c10::Device dev,
-                       hipEvent_t ev, c10::hip::HIPStreamMasqueradingAsCUDA comm, std::shared_ptr<Health> health, bool blocking,
-                       std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc)
+                       hipEvent_t ev, c10::hip::HIPStreamMasqueradingAsCUDA comm, std::shared_ptr<Health> health,
+                       bool blocking, std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc,
+                       std::shared_ptr<EventPool> pool)
     : c10d::Work(rank, type),
       seq_(seq),
       gpu_(true),
@@ -50,21 +43,74 @@ WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at
       ipc_(std::move(ipc)),
       blocking_(blocking),
       timeout_(timeout),
-      start_(std::chrono::steady_clock::now()) {
-  std::vector<c10::Device> devs{dev_};
-  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()), devs);
-  c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm);  // the future's events are recorded on the comm stream
-  fut_->markCompleted(c10::IValue(outputs_));
-}
+      start_(std::chrono::steady_clock::now()),
+      pool_(std::move(pool)),
+      comm_(comm) {}
 
 WorkMI355X::~WorkMI355X() {
-  if (ev_) hipEventDestroy(ev_);
+  if (!ev_) return;
+  if (pool_) pool_->put(ev_);  // re-recording a pooled event later is fine: nobody waits on this one any more
+  else hipEventDestroy(ev_);
 }
 
 void WorkMI355X::done(std::exception_ptr e) {
-  if (e) fut_->setError(e);
-  else fut_->markCompleted(c10::IValue(outputs_));
+  c10::intrusive_ptr<c10::ivalue::Future> f;
+  {
+    std::lock_guard<std::mutex> lk(mutex_);
+    f = fut_;
+  }
   finish(e);
+  if (f) {
+    if (e) f->setError(e);
+    else f->markCompleted(c10::IValue(outputs_));
+  }
+}
+
+c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() {
+  std::unique_lock<std::mutex> lk(mutex_);
+  if (fut_) return fut_;
+  if (gpu_) {
+    fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()),
+                                                    std::vector<c10::Device>{dev_});
+    auto f = fut_;
+    lk.unlock();
+    // the future's own events land on the comm stream after this collective
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(*comm_);
+    f->markCompleted(c10::IValue(outputs_));
+    return f;
+  }
+  fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()));
+  auto f = fut_;
+  const bool done_now = completed_;
+  const std::exception_ptr e = exception_;
+  lk.unlock();
+  if (done_now) {
+    if (e) f->setError(e);
+    else f->markCompleted(c10::IValue(outputs_));
+  }
+  return f;
+}
+
+// =================================================================== EventPool
+hipEvent_t EventPool::get() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!free.empty()) {
+      hipEvent_t e = free.back();
+      free.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e;
+  PDCC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return e;
+}
+void EventPool::put(hipEvent_t e) {
+  std::lock_guard<std::mutex> lk(mu);
+  free.push_back(e);
+}
+EventPool::~EventPool() {
+  for (hipEvent_t e : free) hipEventDestroy(e);
 }
 
 void WorkMI355X::fail(const std::string& msg) {
@@ -126,24 +172,6 @@ bool WorkMI355X::wait(std::chrono::milliseconds timeout) {
 }
 
 std::vector<at::Tensor> WorkMI355X::result() { return outputs_; }
-c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() { return fut_; }
-
-// =================================================================== DeviceState
-hipEvent_t DeviceState::get_event() {
-  std::lock_guard<std::mutex> lk(ev_mu);
-  if (!ev_pool.empty()) {
-    hipEvent_t e = ev_pool.back();
-    ev_pool.pop_back();
-    return e;
-  }
-  hipEvent_t e;
-  PDCC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  return e;
-}
-void DeviceState::put_event(hipEvent_t e) {
-  std::lock_guard<std::mutex> lk(ev_mu);
-  ev_pool.push_back(e);
-}
 
 // =================================================================== helpers
 namespace {
@@ -303,7 +331,6 @@ ProcessGroupMI355X::~ProcessGroupMI355X() {
   for (auto& kv : devs_) {
     DeviceState& ds = *kv.second;
     if (health_->poisoned.load() && ds.rccl) ds.rccl->abort();
-    for (hipEvent_t e : ds.ev_pool) hipEventDestroy(e);
   }
 }
 

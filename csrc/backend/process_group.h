@@ -56,6 +56,15 @@ struct Health {
 
 struct DeviceState;
 
+// Reusable hipEvents (creating one per collective costs a few microseconds).
+struct EventPool {
+  std::mutex mu;
+  std::vector<hipEvent_t> free;
+  hipEvent_t get();
+  void put(hipEvent_t e);
+  ~EventPool();
+};
+
 class WorkMI355X : public c10d::Work {
  public:
   // completed (or failed) CPU work
@@ -65,7 +74,7 @@ class WorkMI355X : public c10d::Work {
   // GPU work: `ev` recorded on the comm stream after the enqueued collective
   WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at::Tensor> outputs, c10::Device dev,
              hipEvent_t ev, c10::hip::HIPStreamMasqueradingAsCUDA comm, std::shared_ptr<Health> health, bool blocking,
-             std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc);
+             std::chrono::milliseconds timeout, std::shared_ptr<IpcComm> ipc, std::shared_ptr<EventPool> pool);
   ~WorkMI355X() override;
 
   bool isCompleted() override;
@@ -95,6 +104,10 @@ class WorkMI355X : public c10d::Work {
   bool blocking_ = false;
   std::chrono::milliseconds timeout_{0};
   std::chrono::steady_clock::time_point start_;
+  std::shared_ptr<EventPool> pool_;
+  std::optional<c10::hip::HIPStreamMasqueradingAsCUDA> comm_;
+  // created lazily in getFuture(): most callers never ask for it, and a
+  // device-aware future records its own events
   c10::intrusive_ptr<c10::ivalue::Future> fut_;
 };
 
@@ -106,11 +119,8 @@ struct DeviceState {
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::unique_ptr<RcclComm> rccl;       // lazy
   std::shared_ptr<IpcComm> ipc;         // lazy
-  std::mutex ev_mu;
-  std::vector<hipEvent_t> ev_pool;
+  std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
   explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
-  hipEvent_t get_event();
-  void put_event(hipEvent_t e);
 };
 
 struct OpStats {

@@ -329,7 +329,9 @@ def dp_train(rank, size, mode="bucketer", steps=5, device="cpu", bucket_bytes=20
         if mode != "torch_ddp":
             buck.finish()
         opt.step()
-    return torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+    # plain floats: a torch tensor sent through an mp.Queue is shared by fd passing,
+    # which races with this process exiting
+    return torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).tolist()
 
 
 def dp_reference(steps=5):

@@ -88,7 +88,7 @@ def test_tutorial_demos_on_shared_gpu(name):
 
 @pytest.mark.parametrize("mode", ["bucketer", "torch_ddp"])
 def test_data_parallel_on_shared_gpu(mode):
-    res = _gpu_launch(W.dp_train, 2, args=(mode, 5, "cuda", 1 << 20))
+    res = [torch.tensor(p) for p in _gpu_launch(W.dp_train, 2, args=(mode, 5, "cuda", 1 << 20))]
     ref = W.dp_reference()
     for p in res:
         torch.testing.assert_close(p, res[0], rtol=0, atol=0)

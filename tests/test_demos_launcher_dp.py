@@ -60,7 +60,7 @@ def test_launcher_propagates_failure(tmp_path):
 
 @pytest.mark.parametrize("mode", ["bucketer", "torch_ddp"])
 def test_data_parallel_matches_single_process(mode):
-    res = launch(W.dp_train, 2, args=(mode,))
+    res = [torch.tensor(p) for p in launch(W.dp_train, 2, args=(mode,))]
     ref = W.dp_reference()
     for p in res:
         torch.testing.assert_close(p, res[0], rtol=0, atol=0)
