@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_BUSBW = {2: 6.14, 4: 5.49, 8: 3.16}  # BASELINE.md §2.1 (reference stack, Gloo/CPU)
+SMALL = os.environ.get("PDCC_BENCH_SMALL", "0") == "1"  # functional rehearsal sizes for the extras
 NBYTES = 1 << 30
 
 
@@ -46,6 +47,10 @@ def main():
     ap.add_argument("--bytes", type=int, default=NBYTES)
     ap.add_argument("--extras", type=int, default=int(os.environ.get("PDCC_BENCH_EXTRAS", "1")))
     args = ap.parse_args()
+    if os.environ.get("PDCC_BENCH_DEBUG_S"):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["PDCC_BENCH_DEBUG_S"]), exit=True)
 
     import torch
     import torch.distributed as dist
@@ -59,6 +64,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    ngpu = torch.cuda.device_count()
+    local = local % ngpu  # (ranks > GPUs only in functional rehearsals on a 1-GPU box)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world == 1:
@@ -87,6 +94,8 @@ def main():
     for _ in range(args.warmup):
         dist.all_reduce(x)
     sync()
+    if rank == 0:
+        print(f"[bench] world={world} warm-up done, timing {args.steps} steps", file=sys.stderr, flush=True)
     # ---- the timed region: exactly K steps
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -208,7 +217,8 @@ def run_extras(world, rank, dev, native, x):
     for algo in ("rccl", "ipc"):
         try:
             gb.set_algo(algo)
-            for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, 1 << 30):
+            progress(f"algo A/B: {algo}")
+            for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, (1 << 30) if not SMALL else (64 << 20)):
                 t = x[: nbytes // 4]
                 lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
                 out[f"allreduce_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
@@ -228,7 +238,100 @@ def run_extras(world, rank, dev, native, x):
         gb.set_algo("auto")
     except Exception:
         pass
+    if "stopped_after" not in out:
+        try:
+            out["baseline_configs"] = baseline_configs(world, rank, dev, x)
+        except Exception as e:
+            out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
     return out
+
+
+def progress(msg):
+    # stderr heartbeat (rank 0): long multi-GPU runs must not look hung
+    import torch.distributed as dist
+
+    if dist.get_rank() == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _p50_coll(fn, iters=5):
+    """BASELINE.md method: barrier + timed collective, max over ranks, median."""
+    import torch
+    import torch.distributed as dist
+
+    fn()
+    lat = []
+    for _ in range(iters):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lat.append(t.item())
+    return statistics.median(lat)
+
+
+def baseline_configs(world, rank, dev, x):
+    """The other BASELINE.json configs on this node (default algorithm selection):
+    six collectives at S = 1 GiB fp32, PRODUCT/MAX/MIN all_reduce at 128 MiB,
+    all_gather bf16 4 GiB/rank (ZeRO-style), all_reduce 256 MiB at w=2."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.utils import busbw as bb
+
+    res = {}
+
+    def rec(name, coll, total_bytes, fn, iters=5, check=None):
+        progress(name)
+        t = _p50_coll(fn, iters)
+        res[name] = {"p50_ms": round(t * 1e3, 3), "busbw_GBps": round(bb(coll, total_bytes, world, t), 1)}
+        if check is not None:
+            res[name]["correct"] = bool(check())
+
+    S = 1 << 30 if not SMALL else 64 << 20
+    n = S // 4
+    chunk = n // world
+    rec("all_reduce_1GiB", "all_reduce", S, lambda: dist.all_reduce(x))
+    rec("reduce_1GiB", "reduce", S, lambda: dist.reduce(x, dst=0))
+    rec("broadcast_1GiB", "broadcast", S, lambda: dist.broadcast(x, src=0))
+    src = torch.full((chunk,), float(rank), device=dev)
+    out = torch.empty(n - n % world, device=dev)
+    rec("all_gather_1GiB", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src),
+        check=lambda: torch.equal(out.view(world, chunk)[:, 0].cpu(), torch.arange(world, dtype=torch.float32)))
+    glist = [torch.empty(chunk, device=dev) for _ in range(world)] if rank == 0 else None
+    rec("gather_1GiB", "gather", S, lambda: dist.gather(src, gather_list=glist, dst=0),
+        check=lambda: rank != 0 or all(bool(glist[r][0].item() == r) for r in range(world)))
+    slist = [torch.full((chunk,), float(r), device=dev) for r in range(world)] if rank == 0 else None
+    sout = torch.empty(chunk, device=dev)
+    rec("scatter_1GiB", "scatter", S, lambda: dist.scatter(sout, scatter_list=slist, src=0),
+        check=lambda: sout[0].item() == rank)
+    del glist, slist
+    rsin = torch.ones(n - n % world, device=dev)
+    rec("reduce_scatter_1GiB", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin),
+        check=lambda: sout[0].item() == world)
+    a2a = torch.empty_like(rsin)
+    rec("all_to_all_1GiB", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin))
+    del rsin, a2a, out, src
+    m = ((128 << 20) if not SMALL else (8 << 20)) // 4
+    for op in ("PRODUCT", "MAX", "MIN"):
+        v = torch.full((m,), 1.0 + 1e-7 * rank, device=dev)
+        rec(f"all_reduce_{op}_128MiB", "all_reduce", 128 << 20,
+            lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op)))
+    del v
+    if world == 2:
+        rec("all_reduce_256MiB", "all_reduce", 256 << 20, lambda: dist.all_reduce(x[: (256 << 20) // 4]))
+    per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
+    ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)
+    ag_out = torch.empty(per * world, dtype=torch.bfloat16, device=dev)
+    rec("all_gather_bf16_4GiB_per_rank", "all_gather", per * 2 * world,
+        lambda: dist.all_gather_into_tensor(ag_out, ag_in), iters=3,
+        check=lambda: torch.equal(ag_out.view(world, per)[:, -1].float().cpu(), torch.arange(world, dtype=torch.float32)))
+    del ag_in, ag_out
+    torch.cuda.empty_cache()
+    return res
 
 
 def _time_local(fn, iters):

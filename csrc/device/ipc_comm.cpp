@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <utility>
 
 #include "comm_util.h"
 
@@ -11,20 +12,40 @@ namespace pdcc {
 
 namespace {
 
+// A hipIpc handle names the runtime's underlying allocation, which may be larger
+// than (and start before) the pointer we exported: the runtime is free to
+// sub-allocate. Export (handle, offset of p from its allocation base) and add the
+// offset back after opening -- without it a second group's buffers would alias
+// the first group's on the peer side.
 std::vector<uint8_t> handle_bytes(void* p) {
   hipIpcMemHandle_t h;
   PDCC_HIP(hipIpcGetMemHandle(&h, p));
-  return std::vector<uint8_t>(reinterpret_cast<uint8_t*>(&h), reinterpret_cast<uint8_t*>(&h) + sizeof(h));
+  hipDeviceptr_t base = nullptr;
+  size_t range = 0;
+  PDCC_HIP(hipMemGetAddressRange(&base, &range, reinterpret_cast<hipDeviceptr_t>(p)));
+  const uint64_t off = static_cast<uint64_t>(static_cast<char*>(p) - static_cast<char*>(base));
+  std::vector<uint8_t> out(sizeof(h) + sizeof(off));
+  std::memcpy(out.data(), &h, sizeof(h));
+  std::memcpy(out.data() + sizeof(h), &off, sizeof(off));
+  return out;
 }
 
-void* open_handle(const std::vector<uint8_t>& b) {
-  if (b.size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("pdcc: malformed hipIpc handle in store");
+// returns {mapping to close later, usable pointer}
+std::pair<void*, void*> open_handle(const std::vector<uint8_t>& b) {
   hipIpcMemHandle_t h;
+  uint64_t off = 0;
+  if (b.size() != sizeof(h) + sizeof(off)) throw std::runtime_error("pdcc: malformed hipIpc handle in store");
   std::memcpy(&h, b.data(), sizeof(h));
+  std::memcpy(&off, b.data() + sizeof(h), sizeof(off));
   void* p = nullptr;
   PDCC_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  return p;
+  return {p, static_cast<char*>(p) + off};
 }
+
+// own allocations in whole 2 MiB granules, so the runtime never packs two of
+// them (or anybody else's) into one IPC-exported allocation
+constexpr size_t kGranule = 2u << 20;
+size_t granule(size_t b) { return (b + kGranule - 1) / kGranule * kGranule; }
 
 struct DeviceScope {
   int prev = 0;
@@ -50,7 +71,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
   DeviceScope ds(device);
-  const size_t sig = kern::ipc_signal_bytes();
+  const size_t sig = granule(kern::ipc_signal_bytes());
   PDCC_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&my_flags_), sig, hipDeviceMallocUncached));
   PDCC_HIP(hipMemset(my_flags_, 0, sig));
   PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
@@ -60,16 +81,24 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
 
   const auto all = store_allgather(store_, key_ + "/ipc_sig", rank_, world_, handle_bytes(my_flags_));
   peer_flags_.assign(world_, nullptr);
-  for (int r = 0; r < world_; ++r)
-    peer_flags_[r] = (r == rank_) ? my_flags_ : static_cast<uint32_t*>(open_handle(all[r]));
+  flags_maps_.assign(world_, nullptr);
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      peer_flags_[r] = my_flags_;
+      continue;
+    }
+    auto m = open_handle(all[r]);
+    flags_maps_[r] = m.first;
+    peer_flags_[r] = static_cast<uint32_t*>(m.second);
+  }
 }
 
 IpcComm::~IpcComm() {
   try {
     DeviceScope ds(device_);
     unmap_staging();
-    for (int r = 0; r < (int)peer_flags_.size(); ++r)
-      if (r != rank_ && peer_flags_[r]) hipIpcCloseMemHandle(peer_flags_[r]);
+    for (void* m : flags_maps_)
+      if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
     if (err_host_) hipHostFree(err_host_);
   } catch (...) {
@@ -77,8 +106,9 @@ IpcComm::~IpcComm() {
 }
 
 void IpcComm::unmap_staging() {
-  for (int r = 0; r < (int)peer_staging_.size(); ++r)
-    if (r != rank_ && peer_staging_[r]) hipIpcCloseMemHandle(peer_staging_[r]);
+  for (void* m : staging_maps_)
+    if (m) hipIpcCloseMemHandle(m);
+  staging_maps_.clear();
   peer_staging_.clear();
   if (my_staging_) hipFree(my_staging_);
   my_staging_ = nullptr;
@@ -86,13 +116,21 @@ void IpcComm::unmap_staging() {
 }
 
 void IpcComm::map_staging(size_t cap) {
-  PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&my_staging_), 2 * cap));
+  PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&my_staging_), granule(2 * cap)));
   cap_ = cap;
   const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_,
                                    handle_bytes(my_staging_));
   peer_staging_.assign(world_, nullptr);
-  for (int r = 0; r < world_; ++r)
-    peer_staging_[r] = (r == rank_) ? my_staging_ : static_cast<char*>(open_handle(all[r]));
+  staging_maps_.assign(world_, nullptr);
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      peer_staging_[r] = my_staging_;
+      continue;
+    }
+    auto m = open_handle(all[r]);
+    staging_maps_[r] = m.first;
+    peer_staging_[r] = static_cast<char*>(m.second);
+  }
 }
 
 void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
@@ -126,8 +164,9 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   v.seq = seq_;
   v.timeout_ticks = timeout_ticks_;
   if (shared_device_) {
-    // all ranks' grids must be co-resident on ONE device (test setups): keep them small
-    call.grid_cap = std::max(1, 64 / world_);
+    // all ranks' grids must be co-resident on ONE device (test setups): stay well
+    // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
+    call.grid_cap = std::max(1, 256 / world_);
   }
   DeviceScope ds(device_);
   PDCC_HIP(kern::ipc_launch(v, call, stream));

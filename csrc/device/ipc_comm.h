@@ -57,12 +57,14 @@ class IpcComm {
 
   uint32_t* my_flags_ = nullptr;          // uncached device memory
   std::vector<uint32_t*> peer_flags_;     // mapped (own entry = my_flags_)
+  std::vector<void*> flags_maps_;         // hipIpcOpenMemHandle results to close (may precede the pointer)
   uint32_t* err_host_ = nullptr;          // pinned, device-visible
   uint32_t* err_dev_ = nullptr;
 
   char* my_staging_ = nullptr;
   size_t cap_ = 0;                         // bytes per parity
   std::vector<char*> peer_staging_;
+  std::vector<void*> staging_maps_;
   int staging_gen_ = 0;
   uint32_t seq_ = 0;
 };

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   echo "=== $name" | tee -a gpurun_out/steps.log
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2> >(tee -a "gpurun_out/$name.err" >&2)
   local rc=$?
   echo "rc=$rc" | tee -a gpurun_out/steps.log
   tail -5 "gpurun_out/$name.log"
@@ -20,6 +20,12 @@ for s in "$@"; do
     backend) step backend 900 python -m pytest tests/test_backend_gpu.py -x -q ;;
     gputests) step gputests 1200 python -m pytest tests -m gpu -q ;;
     bench1) step bench1 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench2dbg) PDCC_BENCH_SMALL=1 PDCC_LOG_LEVEL=2 PDCC_BENCH_DEBUG_S=150 step bench2dbg 240 \
+        python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 --bytes 67108864 ;;
     kprof) step kprof 600 python scripts/kernel_bench.py ;;
+    bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
+        --bytes 67108864 ;;
   esac
 done

@@ -361,3 +361,23 @@ def flight_probe(rank, size):
     dist.broadcast(torch.ones(3), 0)
     b = backend.native_backend()
     return b.flight_recorder(), b.flight_recorder_dump(3)
+
+
+def two_groups(rank, size, device="cuda"):
+    """Two process groups in one process, both on the IPC path, interleaved
+    (regression: the second group's hipIpc mappings must not alias the first's)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    g = dist.new_group(list(range(size)))
+    ok = []
+    for n in (1, 1000, 300_000):
+        a = torch.full((n,), float(rank + 1), device=d)
+        b = torch.full((n,), float(10 * (rank + 1)), device=d)
+        for _ in range(3):
+            dist.all_reduce(a)
+            dist.all_reduce(b, group=g)
+        s = size * (size + 1) / 2
+        ok.append(bool(torch.all(a == s * size ** 2).item()) and bool(torch.all(b == 10 * s * size ** 2).item()))
+    return ok

@@ -93,3 +93,8 @@ def test_data_parallel_on_shared_gpu(mode):
     for p in res:
         torch.testing.assert_close(p, res[0], rtol=0, atol=0)
         torch.testing.assert_close(p, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_two_ipc_groups_in_one_process():
+    for ok in _gpu_launch(W.two_groups, 2, env={"PDCC_ALGO": "ipc"}):
+        assert all(ok), ok
