@@ -174,10 +174,25 @@ struct PipeLds {
   static constexpr int kBytes = DEPTH * NSRC * kTile;
 };
 
+// Wait for tile i (< DEPTH-1) of the prologue: BASE younger loads plus the i
+// stores of the consumes issued since that tile (vmcnt needs an immediate).
+template <int BASE, int DEPTH>
+__device__ __forceinline__ void wait_prologue(int i) {
+  switch (i) {
+    case 0: wait_vmcnt<BASE>(); break;
+    case 1: if constexpr (DEPTH > 2) wait_vmcnt<BASE + 1>(); break;
+    case 2: if constexpr (DEPTH > 3) wait_vmcnt<BASE + 2>(); break;
+    case 3: if constexpr (DEPTH > 4) wait_vmcnt<BASE + 3>(); break;
+    case 4: if constexpr (DEPTH > 5) wait_vmcnt<BASE + 4>(); break;
+    case 5: if constexpr (DEPTH > 6) wait_vmcnt<BASE + 5>(); break;
+    default: if constexpr (DEPTH > 7) wait_vmcnt<BASE + 6>(); break;
+  }
+}
+
 template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   static_assert((DEPTH - 1) * (NSRC + 1) < 64, "pipeline too deep for vmcnt");
-  static_assert(DEPTH >= 2 && DEPTH <= 4, "prologue wait counts are written out for DEPTH <= 4");
+  static_assert(DEPTH >= 2 && DEPTH <= 8, "prologue wait counts are written out for DEPTH <= 8");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const uint32_t lane_off = wave * kWaveBytes + lane * 16;
@@ -232,12 +247,8 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
     // last load still be in flight when its LDS slot is read).
     if (i >= (size_t)(DEPTH - 1)) {
       wait_vmcnt<(DEPTH - 1) * (NSRC + 1)>();
-    } else if (i == 0) {
-      wait_vmcnt<(DEPTH - 1) * NSRC>();
-    } else if (i == 1) {
-      wait_vmcnt<(DEPTH - 1) * NSRC + (DEPTH > 2 ? 1 : 0)>();
     } else {
-      wait_vmcnt<(DEPTH - 1) * NSRC + (DEPTH > 3 ? 2 : 0)>();
+      wait_prologue<(DEPTH - 1) * NSRC, DEPTH>((int)i);
     }
     consume(i, stage);
     stage = (stage + 1 == DEPTH) ? 0 : stage + 1;

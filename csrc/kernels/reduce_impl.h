@@ -3,6 +3,8 @@
 // which instantiates PDCC_REDUCE_DTYPE(<dt>) -- 8 small TUs that hipcc builds in
 // parallel instead of one huge one.
 #pragma once
+#include <cstdlib>
+
 #include "dev_common.h"
 
 namespace pdcc {
@@ -14,6 +16,7 @@ using kern::IpcView;
 
 struct Ptrs8 {
   const char* p[kern::kMaxRanks];
+  int chunked;  // K1 tile->block map: 0 = strided (block b: b, b+G, ...), 1 = contiguous run per block
 };
 
 // LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU)
@@ -50,18 +53,34 @@ __device__ __forceinline__ void reduce_tail(const char* const* s, char* d, size_
   else store_partial(d + off, r, lim);
 }
 
-template <DType DT, RedOp OP, int NSRC>
+__device__ __forceinline__ StridedMap k1_map(const Ptrs8& s, char* dst, size_t nbytes) {
+  const size_t nt = nbytes / kTile;
+  if (s.chunked) {
+    const size_t per = (nt + gridDim.x - 1) / gridDim.x;
+    const size_t b0 = blockIdx.x * per;
+    return StridedMap{s.p, dst, b0, 1, b0 + per < nt ? b0 + per : nt};
+  }
+  return StridedMap{s.p, dst, blockIdx.x, gridDim.x, nt};
+}
+
+// K1 runs one 256-thread workgroup per CU (measured fastest for streaming), so
+// it can afford a deeper LDS ring than the IPC kernels (which want 2 per CU).
+template <int NSRC>
+struct K1Deep {
+  static constexpr int value = NSRC <= 2 ? 6 : (NSRC <= 4 ? 4 : 3);
+};
+
+template <DType DT, RedOp OP, int NSRC, int D>
 __global__ void __launch_bounds__(256) k1_reduce_lds(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
-  constexpr int D = DepthFor<NSRC>::value;
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<NSRC, D>::kBytes];
-  const StridedMap m{srcs.p, dst, blockIdx.x, gridDim.x, nbytes / kTile};
+  const StridedMap m = k1_map(srcs, dst, nbytes);
   pipe_run<DT, OP, NSRC, D>(lds, m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
 
 template <DType DT, RedOp OP, int NSRC>
 __global__ void __launch_bounds__(256) k1_reduce_regs(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
-  const StridedMap m{srcs.p, dst, blockIdx.x, gridDim.x, nbytes / kTile};
+  const StridedMap m = k1_map(srcs, dst, nbytes);
   pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2)>(m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
@@ -181,8 +200,14 @@ hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_
                      bool lds) {
   Ptrs8 p{};
   for (int k = 0; k < NSRC; ++k) p.p[k] = (const char*)srcs[k];
+  static const int chunked = [] {
+    const char* e = getenv("PDCC_K1_CHUNKED");
+    return e && *e == '1' ? 1 : 0;
+  }();
+  p.chunked = chunked;
   if (lds)
-    hipLaunchKernelGGL((k1_reduce_lds<DT, OP, NSRC>), dim3(grid), dim3(256), 0, s, p, (char*)out, nbytes, avg_div);
+    hipLaunchKernelGGL((k1_reduce_lds<DT, OP, NSRC, K1Deep<NSRC>::value>), dim3(grid), dim3(256), 0, s, p, (char*)out,
+                       nbytes, avg_div);
   else
     hipLaunchKernelGGL((k1_reduce_regs<DT, OP, NSRC>), dim3(grid), dim3(256), 0, s, p, (char*)out, nbytes, avg_div);
   return hipGetLastError();
