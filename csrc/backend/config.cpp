@@ -60,6 +60,14 @@ Config Config::from_env() {
   c.ipc_max_staging = env_size("PDCC_IPC_MAX_STAGING", c.ipc_max_staging);
   c.ipc_enable = env_bool("PDCC_IPC", c.ipc_enable);
   c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
+  if (const char* sm = env("PDCC_STREAM")) {
+    std::string v(sm);
+    if (v == "auto") c.stream_mode = 0;
+    else if (v == "high") c.stream_mode = 1;
+    else if (v == "comm") c.stream_mode = 2;
+    else if (v == "current") c.stream_mode = 3;
+    else throw std::runtime_error("PDCC_STREAM must be auto|high|comm|current, got " + v);
+  }
   c.shm_slot_bytes = env_size("PDCC_SHM_SLOT_BYTES", c.shm_slot_bytes);
   c.shm_chan_bytes = env_size("PDCC_SHM_CHAN_BYTES", c.shm_chan_bytes);
   c.debug = env_bool("PDCC_DEBUG", c.debug);
@@ -77,7 +85,7 @@ std::string Config::describe() const {
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
-    << " watchdog_ms=" << watchdog_ms;
+    << " watchdog_ms=" << watchdog_ms << " stream=" << (stream_mode == 0 ? "auto" : stream_mode == 1 ? "high" : stream_mode == 2 ? "comm" : "current");
   return o.str();
 }
 

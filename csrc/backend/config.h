@@ -19,6 +19,12 @@ struct Config {
   size_t ipc_copy_max = 1u << 20;          // PDCC_IPC_COPY_MAX    broadcast/gather/... <= this: IPC
   size_t ipc_max_staging = 512u << 20;     // PDCC_IPC_MAX_STAGING per parity; larger messages are chunked
   bool ipc_enable = true;                  // PDCC_IPC=0 disables the peer-memory path
+  // PDCC_STREAM: auto (default) = synchronous collectives (async_op=False) on the caller's stream,
+  // async ones on a normal-priority comm stream; high = auto with a high-priority comm stream;
+  // comm = always the comm stream; current = always the caller's stream.
+  // (Measured on MI355X: a cross-stream event hand-off costs ~20 us per op on a normal
+  // stream and ~150 us on a high-priority one; the caller's stream ~5 us end to end.)
+  int stream_mode = 0;
   bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
   // host transport
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES

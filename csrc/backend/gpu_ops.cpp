@@ -159,7 +159,8 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
   for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
 
-  auto ds = std::make_unique<DeviceState>(c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/true, (c10::DeviceIndex)d));
+  auto ds = std::make_unique<DeviceState>(
+      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
   ds->device = d;
   ds->shared_device = shared;
   ds->rccl_ok = !shared;
@@ -233,24 +234,33 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
                                                            std::shared_ptr<IpcComm> ipcp) {
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
-  hipEvent_t pre = ds.events->get();
-  PDCC_HIP(hipEventRecord(pre, cur.stream()));
-  PDCC_HIP(hipStreamWaitEvent(ds.stream.stream(), pre, 0));
-  ds.events->put(pre);
+  // synchronous collectives (and PDCC_STREAM=current) run on the caller's stream: no
+  // cross-stream event hand-off, which costs far more than the launch on this runtime
+  const bool on_current = cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_);
+  const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : ds.stream;
+  if (comm != cur) {
+    hipEvent_t pre = ds.events->get();
+    PDCC_HIP(hipEventRecord(pre, cur.stream()));
+    PDCC_HIP(hipStreamWaitEvent(comm.stream(), pre, 0));
+    ds.events->put(pre);
+  }
   const bool rx = cfg_.roctx && roctx_push_;
   if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
   {
-    c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);  // temporaries + copy-backs run on the comm stream
-    fn(ds.stream.stream());
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(comm);  // temporaries + copy-backs run on the comm stream
+    fn(comm.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
-  for (const auto& t : keep_alive)
-    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), ds.stream);
-  for (const auto& t : outputs)
-    if (t.defined() && t.is_cuda()) c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), ds.stream);
-  hipEvent_t ev;
-  ev = ds.events->get();
-  PDCC_HIP(hipEventRecord(ev, ds.stream.stream()));
+  if (comm != cur) {  // the caching allocator must not recycle these before the comm stream is done
+    for (const auto& t : keep_alive)
+      if (t.defined() && t.is_cuda())
+        c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), comm);
+    for (const auto& t : outputs)
+      if (t.defined() && t.is_cuda())
+        c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), comm);
+  }
+  hipEvent_t ev = ds.events->get();
+  PDCC_HIP(hipEventRecord(ev, comm.stream()));
   auto w = c10::make_intrusive<WorkMI355X>(rank_, [c] {
     switch (c) {
       case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
@@ -265,7 +275,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
       case Coll::RECV: return c10d::OpType::RECV;
       default: return c10d::OpType::BARRIER;
     }
-  }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, ds.stream,
+  }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, comm,
                                            health_, cfg_.blocking_wait, timeout, std::move(ipcp), ds.events);
   if (cfg_.watchdog_ms > 0) {
     std::lock_guard<std::mutex> lk(wd_mu_);

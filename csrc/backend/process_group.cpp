@@ -95,9 +95,9 @@ c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() {
 hipEvent_t EventPool::get() {
   {
     std::lock_guard<std::mutex> lk(mu);
-    if (!free.empty()) {
-      hipEvent_t e = free.back();
-      free.pop_back();
+    if (free.size() > 8) {  // FIFO with slack: re-record the least recently used event
+      hipEvent_t e = free.front();
+      free.pop_front();
       return e;
     }
   }
@@ -150,6 +150,7 @@ void WorkMI355X::synchronize() {
   if (!gpu_) return;
   c10::hip::HIPGuardMasqueradingAsCUDA g(dev_);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev_.index());
+  if (comm_ && *comm_ == cur) return;  // enqueued on this very stream: already ordered
   PDCC_HIP(hipStreamWaitEvent(cur.stream(), ev_, 0));
 }
 
@@ -596,6 +597,7 @@ void ProcessGroupMI355X::p2p_submit(bool is_send, Job j) {
 // =================================================================== collectives
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce(std::vector<at::Tensor>& tensors,
                                                              const c10d::AllreduceOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(tensors, "allreduce");
   at::Tensor& t = tensors[0];
   before_op(Coll::ALLREDUCE, tensors, -1);
@@ -619,6 +621,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce_coalesced(std::vect
     c10d::AllreduceOptions o;
     o.reduceOp = opts.reduceOp;
     o.timeout = opts.timeout;
+    o.asyncOp = opts.asyncOp;
     last = allreduce(one, o);
   }
   if (!last) return cpu_done(Coll::ALLREDUCE, {});
@@ -628,6 +631,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce_coalesced(std::vect
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce(std::vector<at::Tensor>& tensors,
                                                           const c10d::ReduceOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(tensors, "reduce");
   check_root(opts.rootRank, size_, "reduce");
   at::Tensor& t = tensors[0];
@@ -647,6 +651,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce(std::vector<at::Tensor
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::broadcast(std::vector<at::Tensor>& tensors,
                                                              const c10d::BroadcastOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(tensors, "broadcast");
   check_root(opts.rootRank, size_, "broadcast");
   at::Tensor& t = tensors[0];
@@ -665,6 +670,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::broadcast(std::vector<at::Ten
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather(std::vector<std::vector<at::Tensor>>& outputs,
                                                              std::vector<at::Tensor>& inputs,
                                                              const c10d::AllgatherOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(inputs, "allgather");
   TORCH_CHECK(outputs.size() == 1, "ProcessGroupMI355X::allgather: expects one output list");
   at::Tensor& in = inputs[0];
@@ -709,6 +715,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather_into_tensor_coalesc
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gather(std::vector<std::vector<at::Tensor>>& outputs,
                                                           std::vector<at::Tensor>& inputs,
                                                           const c10d::GatherOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(inputs, "gather");
   check_root(opts.rootRank, size_, "gather");
   at::Tensor& in = inputs[0];
@@ -740,6 +747,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gather(std::vector<std::vecto
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::scatter(std::vector<at::Tensor>& outputs,
                                                            std::vector<std::vector<at::Tensor>>& inputs,
                                                            const c10d::ScatterOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(outputs, "scatter");
   check_root(opts.rootRank, size_, "scatter");
   at::Tensor& out = outputs[0];
@@ -771,6 +779,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::scatter(std::vector<at::Tenso
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter(std::vector<at::Tensor>& outputs,
                                                                   std::vector<std::vector<at::Tensor>>& inputs,
                                                                   const c10d::ReduceScatterOptions& opts) {
+  op_async_ = opts.asyncOp;
   check_single(outputs, "reduce_scatter");
   TORCH_CHECK(inputs.size() == 1, "ProcessGroupMI355X::reduce_scatter: expects one input list");
   at::Tensor& out = outputs[0];
@@ -818,6 +827,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall_base(at::Tensor& out
                                                                  std::vector<int64_t>& output_splits,
                                                                  std::vector<int64_t>& input_splits,
                                                                  const c10d::AllToAllOptions& opts) {
+  op_async_ = opts.asyncOp;
   TORCH_CHECK(input.is_contiguous() && output.is_contiguous(), "ProcessGroupMI355X::alltoall_base: contiguous tensors only");
   TORCH_CHECK(input.scalar_type() == output.scalar_type(), "ProcessGroupMI355X::alltoall_base: dtype mismatch");
   const bool equal = output_splits.empty() && input_splits.empty();
@@ -863,6 +873,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall_base(at::Tensor& out
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall(std::vector<at::Tensor>& outputs,
                                                             std::vector<at::Tensor>& inputs,
                                                             const c10d::AllToAllOptions& opts) {
+  op_async_ = opts.asyncOp;
   TORCH_CHECK((int)outputs.size() == size_ && (int)inputs.size() == size_,
               "ProcessGroupMI355X::alltoall: expects one input and one output tensor per rank");
   before_op(Coll::ALLTOALL, inputs, -1);
@@ -886,6 +897,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall(std::vector<at::Tens
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::send(std::vector<at::Tensor>& tensors, int dst, int tag) {
+  op_async_ = true;  // p2p pairs must be able to overlap: comm stream
   check_single(tensors, "send");
   TORCH_CHECK(dst >= 0 && dst < size_ && dst != rank_, "ProcessGroupMI355X::send: invalid destination rank ", dst);
   before_op(Coll::SEND, tensors, dst);
@@ -901,6 +913,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::send(std::vector<at::Tensor>&
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::recv(std::vector<at::Tensor>& tensors, int src, int tag) {
+  op_async_ = true;  // p2p pairs must be able to overlap: comm stream
   check_single(tensors, "recv");
   TORCH_CHECK(src >= 0 && src < size_ && src != rank_, "ProcessGroupMI355X::recv: invalid source rank ", src);
   before_op(Coll::RECV, tensors, src);
@@ -924,7 +937,12 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::barrier(const c10d::BarrierOp
   const auto t0 = std::chrono::steady_clock::now();
   {
     std::lock_guard<std::mutex> lk(init_mu_);
-    for (auto& kv : devs_) PDCC_HIP(hipStreamSynchronize(kv.second->stream.stream()));
+    for (auto& kv : devs_) {
+      PDCC_HIP(hipStreamSynchronize(kv.second->stream.stream()));
+      // synchronous collectives were enqueued on the caller's stream
+      PDCC_HIP(hipStreamSynchronize(
+            c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)kv.first).stream()));
+    }
   }
   if (size_ > 1) {
     if (same_host_) shm().barrier(eff_timeout(opts.timeout));

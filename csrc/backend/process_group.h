@@ -59,7 +59,7 @@ struct DeviceState;
 // Reusable hipEvents (creating one per collective costs a few microseconds).
 struct EventPool {
   std::mutex mu;
-  std::vector<hipEvent_t> free;
+  std::deque<hipEvent_t> free;
   hipEvent_t get();
   void put(hipEvent_t e);
   ~EventPool();
@@ -113,7 +113,7 @@ class WorkMI355X : public c10d::Work {
 
 struct DeviceState {
   int device = -1;
-  c10::hip::HIPStreamMasqueradingAsCUDA stream;           // high-priority comm stream
+  c10::hip::HIPStreamMasqueradingAsCUDA stream;  // comm stream for async collectives (PDCC_STREAM)
   bool rccl_ok = false;                 // all ranks on distinct devices
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
   bool shared_device = false;           // several ranks share one GPU (test setups)
@@ -266,6 +266,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::map<int, std::unique_ptr<DeviceState>> devs_;
 
   std::atomic<uint64_t> op_seq_{0};
+  bool op_async_ = true;  // asyncOp of the collective being issued (front-end async_op=...)
   int fault_rank_ = -1;
   uint64_t fault_seq_ = 0;
   std::string fault_kind_;
