@@ -238,11 +238,31 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   // cross-stream event hand-off, which costs far more than the launch on this runtime
   const bool on_current = cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_);
   const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : ds.stream;
+  StreamSync& sy = *ds.sync;
+  bool use_sig = false;
   if (comm != cur) {
-    hipEvent_t pre = ds.events->get();
-    PDCC_HIP(hipEventRecord(pre, cur.stream()));
-    PDCC_HIP(hipStreamWaitEvent(comm.stream(), pre, 0));
-    ds.events->put(pre);
+    {
+      std::lock_guard<std::mutex> lk(sy.mu);  // tick + enqueue under one lock: words only ever grow
+      if (sy.ok && !sy.comm_done.ptr) sy.comm_done.ptr = sy.alloc();
+      if (sy.ok) {
+        SignalWord& w = sy.user_ready[cur.stream()];
+        if (!w.ptr) w.ptr = sy.alloc();
+        if (w.ptr) {
+          const uint64_t t = ++w.next;
+          PDCC_HIP(hipStreamWriteValue64(cur.stream(), w.ptr, t, 0));
+          PDCC_HIP(hipStreamWaitValue64(comm.stream(), w.ptr, t, hipStreamWaitValueGte, ~0ull));
+          use_sig = true;
+        } else {
+          sy.user_ready.erase(cur.stream());
+        }
+      }
+    }
+    if (!use_sig) {
+      hipEvent_t pre = ds.events->get();
+      PDCC_HIP(hipEventRecord(pre, cur.stream()));
+      PDCC_HIP(hipStreamWaitEvent(comm.stream(), pre, 0));
+      ds.events->put(pre);
+    }
   }
   const bool rx = cfg_.roctx && roctx_push_;
   if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
@@ -259,8 +279,16 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
       if (t.defined() && t.is_cuda())
         c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(t.storage().data_ptr(), comm);
   }
-  hipEvent_t ev = ds.events->get();
-  PDCC_HIP(hipEventRecord(ev, comm.stream()));
+  hipEvent_t ev = nullptr;
+  uint64_t done_tick = 0;
+  if (use_sig) {
+    std::lock_guard<std::mutex> lk(sy.mu);
+    done_tick = ++sy.comm_done.next;
+    PDCC_HIP(hipStreamWriteValue64(comm.stream(), sy.comm_done.ptr, done_tick, 0));
+  } else {
+    ev = ds.events->get();
+    PDCC_HIP(hipEventRecord(ev, comm.stream()));
+  }
   auto w = c10::make_intrusive<WorkMI355X>(rank_, [c] {
     switch (c) {
       case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
@@ -277,6 +305,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
     }
   }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, comm,
                                            health_, cfg_.blocking_wait, timeout, std::move(ipcp), ds.events);
+  if (use_sig) w->set_signal(ds.sync, sy.comm_done.ptr, done_tick);
   if (cfg_.watchdog_ms > 0) {
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.emplace_back(w);

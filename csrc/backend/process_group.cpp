@@ -91,6 +91,28 @@ c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() {
   return f;
 }
 
+// =================================================================== StreamSync
+uint64_t* StreamSync::alloc() {
+  if (!ok) return nullptr;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    ok = false;
+    return nullptr;
+  }
+  if (hipMemset(p, 0, sizeof(uint64_t)) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(p);
+    ok = false;
+    return nullptr;
+  }
+  return static_cast<uint64_t*>(p);
+}
+StreamSync::~StreamSync() {
+  if (comm_done.ptr) (void)hipFree(comm_done.ptr);
+  for (auto& kv : user_ready) (void)hipFree(kv.second.ptr);
+}
+
 // =================================================================== EventPool
 hipEvent_t EventPool::get() {
   {
@@ -119,6 +141,7 @@ void WorkMI355X::fail(const std::string& msg) {
 }
 
 bool WorkMI355X::gpu_event_done() {
+  if (done_word_) return __atomic_load_n(done_word_, __ATOMIC_ACQUIRE) >= done_value_;
   if (!ev_) return true;
   return hipEventQuery(ev_) == hipSuccess;
 }
@@ -151,6 +174,11 @@ void WorkMI355X::synchronize() {
   c10::hip::HIPGuardMasqueradingAsCUDA g(dev_);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev_.index());
   if (comm_ && *comm_ == cur) return;  // enqueued on this very stream: already ordered
+  if (done_word_) {
+    PDCC_HIP(hipStreamWaitValue64(cur.stream(), const_cast<uint64_t*>(done_word_), done_value_,
+                                  hipStreamWaitValueGte, ~0ull));
+    return;
+  }
   PDCC_HIP(hipStreamWaitEvent(cur.stream(), ev_, 0));
 }
 

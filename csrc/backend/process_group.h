@@ -65,6 +65,25 @@ struct EventPool {
   ~EventPool();
 };
 
+// Cross-stream ordering with stream memory operations instead of hipEvents:
+// the producer stream writes a monotonic tick into an 8-byte signal-memory word
+// (hipStreamWriteValue64), the consumer stream waits for >= tick
+// (hipStreamWaitValue64). Measured on MI355X: ~5 us per hop vs ~10 us for
+// hipEventRecord + hipStreamWaitEvent; the word is host-readable, so completion
+// queries need no event either.
+struct SignalWord {
+  uint64_t* ptr = nullptr;
+  uint64_t next = 0;
+};
+struct StreamSync {
+  std::mutex mu;
+  bool ok = true;                                // false: runtime lacks signal memory -> events
+  SignalWord comm_done;                          // written by the comm stream after each async op
+  std::map<hipStream_t, SignalWord> user_ready;  // written by each caller stream before an async op
+  uint64_t* alloc();                             // nullptr when unavailable
+  ~StreamSync();
+};
+
 class WorkMI355X : public c10d::Work {
  public:
   // completed (or failed) CPU work
@@ -85,6 +104,12 @@ class WorkMI355X : public c10d::Work {
   c10::intrusive_ptr<c10::ivalue::Future> getFuture() override;
   uint64_t getSequencenumber() const override { return seq_; }
 
+  // async GPU work ordered by a signal word instead of an event
+  void set_signal(std::shared_ptr<StreamSync> sync, const uint64_t* word, uint64_t value) {
+    sync_ = std::move(sync);
+    done_word_ = word;
+    done_value_ = value;
+  }
   void done(std::exception_ptr e);  // CPU async completion
   bool gpu() const { return gpu_; }
   bool gpu_event_done();
@@ -105,6 +130,9 @@ class WorkMI355X : public c10d::Work {
   std::chrono::milliseconds timeout_{0};
   std::chrono::steady_clock::time_point start_;
   std::shared_ptr<EventPool> pool_;
+  std::shared_ptr<StreamSync> sync_;
+  const uint64_t* done_word_ = nullptr;
+  uint64_t done_value_ = 0;
   std::optional<c10::hip::HIPStreamMasqueradingAsCUDA> comm_;
   // created lazily in getFuture(): most callers never ask for it, and a
   // device-aware future records its own events
@@ -120,6 +148,7 @@ struct DeviceState {
   std::unique_ptr<RcclComm> rccl;       // lazy
   std::shared_ptr<IpcComm> ipc;         // lazy
   std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
+  std::shared_ptr<StreamSync> sync = std::make_shared<StreamSync>();
   explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
 };
 

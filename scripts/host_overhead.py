@@ -5,7 +5,9 @@
     python scripts/host_overhead.py nccl     # torch's ProcessGroupNCCL (same RCCL underneath)
 
 Reports the host-side enqueue time per all_reduce (4 B) and the end-to-end
-time per call including the GPU (both averaged over 2000 calls).
+time per call including the GPU (both averaged over 2000 calls), for the
+synchronous form and for ``async_op=True`` followed by ``Work.wait()`` (which
+crosses to the backend's comm stream and back).
 """
 import datetime
 import json
@@ -40,8 +42,17 @@ def main():
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    print(json.dumps({"backend": backend, "enqueue_us": round((t1 - t0) / n * 1e6, 2),
-                      "end_to_end_us": round((t2 - t0) / n * 1e6, 2)}))
+    t3 = time.perf_counter()
+    for _ in range(n):
+        dist.all_reduce(t, async_op=True).wait()
+    t4 = time.perf_counter()
+    torch.cuda.synchronize()
+    t5 = time.perf_counter()
+    print(json.dumps({"backend": backend, "stream": os.environ.get("PDCC_STREAM", "auto"),
+                      "enqueue_us": round((t1 - t0) / n * 1e6, 2),
+                      "end_to_end_us": round((t2 - t0) / n * 1e6, 2),
+                      "async_wait_enqueue_us": round((t4 - t3) / n * 1e6, 2),
+                      "async_wait_end_to_end_us": round((t5 - t3) / n * 1e6, 2)}))
     dist.destroy_process_group()
 
 

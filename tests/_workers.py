@@ -381,3 +381,39 @@ def two_groups(rank, size, device="cuda"):
         s = size * (size + 1) / 2
         ok.append(bool(torch.all(a == s * size ** 2).item()) and bool(torch.all(b == 10 * s * size ** 2).item()))
     return ok
+
+
+def async_ordering(rank, size, device="cuda", rounds=20):
+    """async_op=True collectives run on the backend's comm stream: the hand-off
+    from the caller's stream (producer kernels still running) and back (Work.wait
+    / is_completed polling / futures) must order correctly."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ok = []
+    m = torch.randn(1024, 1024, device=d)
+    for i in range(rounds):
+        x = torch.zeros(1 << 18, device=d)
+        for _ in range(4):  # keep the caller's stream busy before the producer write lands
+            m = torch.tanh(m @ m)
+        x.add_(float(rank + 1 + i) + 0 * m[0, 0])
+        w = dist.all_reduce(x, async_op=True)
+        if i % 3 == 0:
+            w.wait()
+        elif i % 3 == 1:
+            while not w.is_completed():
+                pass
+            w.wait()
+        else:
+            w.get_future().wait()
+        exp = sum(r + 1 + i for r in range(size))
+        ok.append(bool(torch.all(x == exp).item()))
+    # several in flight at once, then wait them in reverse
+    xs = [torch.full((1000 * (k + 1),), float(k + rank), device=d) for k in range(6)]
+    ws = [dist.all_reduce(t, async_op=True) for t in xs]
+    for w in reversed(ws):
+        w.wait()
+    for k, t in enumerate(xs):
+        ok.append(bool(torch.all(t == sum(k + r for r in range(size))).item()))
+    return ok

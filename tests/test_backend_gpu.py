@@ -98,3 +98,12 @@ def test_data_parallel_on_shared_gpu(mode):
 def test_two_ipc_groups_in_one_process():
     for ok in _gpu_launch(W.two_groups, 2, env={"PDCC_ALGO": "ipc"}):
         assert all(ok), ok
+
+
+@pytest.mark.parametrize("world,stream", [(1, "auto"), (1, "comm"), (2, "auto"), (2, "comm")])
+def test_async_ops_stream_ordering(world, stream):
+    env = {"PDCC_STREAM": stream, "PDCC_WORLD1_LOCAL": "0"}
+    if world > 1:
+        env["PDCC_ALGO"] = "ipc"
+    for ok in _gpu_launch(W.async_ordering, world, env=env):
+        assert all(ok), ok
