@@ -70,6 +70,7 @@ Config Config::from_env() {
   }
   c.shm_slot_bytes = env_size("PDCC_SHM_SLOT_BYTES", c.shm_slot_bytes);
   c.shm_chan_bytes = env_size("PDCC_SHM_CHAN_BYTES", c.shm_chan_bytes);
+  c.shm_spin_us = (int)env_int("PDCC_SHM_SPIN_US", c.shm_spin_us);
   c.debug = env_bool("PDCC_DEBUG", c.debug);
   c.log_level = env_int("PDCC_LOG_LEVEL", c.log_level);
   c.blocking_wait = env_bool("PDCC_BLOCKING_WAIT", c.blocking_wait);

@@ -29,6 +29,7 @@ struct Config {
   // host transport
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES
   size_t shm_chan_bytes = 1u << 20;        // PDCC_SHM_CHAN_BYTES
+  int shm_spin_us = 300;                   // PDCC_SHM_SPIN_US (busy-wait window before futex sleep)
   // robustness / observability
   bool debug = false;                      // PDCC_DEBUG=1: cross-rank op fingerprint check
   int log_level = 0;                       // PDCC_LOG_LEVEL 0 quiet, 1 info, 2 every collective

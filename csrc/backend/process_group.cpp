@@ -373,6 +373,7 @@ host::ShmComm& ProcessGroupMI355X::shm() {
     TORCH_CHECK(same_host_, "pdcc: the shared-memory host path needs every rank of the group on one host");
     host::ShmConfig sc;
     sc.slot_bytes = cfg_.shm_slot_bytes;
+    sc.spin_us = cfg_.shm_spin_us;
     sc.chan_bytes = size_ > 16 ? std::min<size_t>(cfg_.shm_chan_bytes, 256u << 10) : cfg_.shm_chan_bytes;
     sc.timeout = timeout_;
     shm_ = std::make_unique<host::ShmComm>(store_, "pdcc/shm", rank_, size_, sc);

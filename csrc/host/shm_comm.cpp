@@ -166,6 +166,10 @@ ShmComm::ShmComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     h->pids[rank] = getpid();
     h->attached.v.fetch_add(1, std::memory_order_acq_rel);
   }
+  // more ranks than CPUs on this host: spinning steals the CPU a peer needs
+  const long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+  oversub_ = ncpu > 0 && world > ncpu;
+  spin_us_ = oversub_ ? std::min(cfg_.spin_us, 20) : cfg_.spin_us;
   // everybody attached and published its pid
   barrier(cfg_.timeout);
   peer_pids_.assign(hdr()->pids, hdr()->pids + world);
@@ -200,11 +204,15 @@ void ShmComm::check_peers(const char* what) {
 template <class Pred>
 void ShmComm::wait_until(Pred pred, std::atomic<uint32_t>* fw, uint32_t fval, std::chrono::milliseconds timeout,
                          const char* what) {
-  for (int i = 0; i < 2048; ++i) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0;; ++i) {
     if (pred()) return;
     _mm_pause();
+    if ((i & 63) == 63) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
+      if (oversub_) std::this_thread::yield();
+    }
   }
-  const auto t0 = std::chrono::steady_clock::now();
   auto last_check = t0;
   while (!pred()) {
     if (fw) futex_wait(fw, fval, 200000);  // 200 us

@@ -33,6 +33,10 @@ constexpr int kMaxShmRanks = 64;
 struct ShmConfig {
   size_t slot_bytes = 8u << 20;   // per-rank staging slot per set
   size_t chan_bytes = 1u << 20;   // per directed pair p2p ring
+  // busy-wait window before a waiter sleeps on the futex: must cover the usual
+  // arrival skew between ranks (tens of us), or every op pays a ~100 us wake-up.
+  // Shortened automatically when ranks outnumber the CPUs.
+  int spin_us = 300;
   std::chrono::milliseconds timeout{std::chrono::minutes(30)};
 };
 
@@ -93,6 +97,8 @@ class ShmComm {
 
   int rank_;
   int world_;
+  int spin_us_ = 300;
+  bool oversub_ = false;
   ShmConfig cfg_;
   std::string name_;
   void* base_ = nullptr;

@@ -15,6 +15,8 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
+| PDCC_SHM_SPIN_US | 300 | host transport busy-wait window before a futex sleep (20 when ranks > CPUs) |
+| PDCC_STREAM | auto | GPU stream policy: auto (sync ops on the caller's stream, async on a comm stream), high, comm, current |
 | PDCC_DEBUG | 0 | cross-rank fingerprint check before every collective |
 | PDCC_LOG_LEVEL | 0 | 1: group/device info, 2: every collective |
 | PDCC_BLOCKING_WAIT | 0 | ``Work.wait()`` blocks the host until the GPU op finished |
@@ -55,6 +57,8 @@ class Config:
     world1_local: bool = True
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
+    shm_spin_us: int = 300
+    stream: str = "auto"
     debug: bool = False
     log_level: int = 0
     blocking_wait: bool = False
@@ -68,7 +72,8 @@ _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "world1_local": "PDCC_WORLD1_LOCAL",
-    "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES", "debug": "PDCC_DEBUG",
+    "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
+    "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
     "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",
     "watchdog_ms": "PDCC_WATCHDOG_MS", "flight_recorder": "PDCC_FLIGHT_RECORDER", "fault": "PDCC_FAULT",
 }
@@ -92,6 +97,8 @@ def current(environ=None) -> Config:
             setattr(c, f.name, _parse(f.type, raw))
     if c.algo not in ("auto", "rccl", "ipc", "host"):
         raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|host, got {c.algo!r}")
+    if c.stream not in ("auto", "high", "comm", "current"):
+        raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     return c
 
 
