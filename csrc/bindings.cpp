@@ -70,7 +70,7 @@ void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std
   TORCH_CHECK(e == hipSuccess, "reduce_nway launch failed: ", hipGetErrorString(e));
 }
 
-void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, int max_blocks, int depth) {
   TORCH_CHECK(srcs.size() == dsts.size(), "multi_copy: list length mismatch");
   if (srcs.empty()) return;
   std::vector<pdcc::kern::CopyDesc> d;
@@ -84,7 +84,7 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(srcs[0].device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(srcs[0].device().index()).stream();
-  hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s);
+  hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s, max_blocks, depth);
   TORCH_CHECK(e == hipSuccess, "multi_copy launch failed: ", hipGetErrorString(e));
 }
 
@@ -138,7 +138,8 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
         py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");
-  m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), "K2: one-launch multi-tensor copy");
+  m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
+        "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);
   m.attr("MAX_RANKS_IPC") = pdcc::kern::kMaxRanks;
   m.attr("TILE_BYTES") = pdcc::kern::kTileBytes;

@@ -42,10 +42,11 @@ struct DescMap {
   __device__ size_t valid(size_t) const { return kTile; }
 };
 
+template <int D>
 __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, D>::kBytes];
   const DescMap m{&a, blockIdx.x, gridDim.x, a.prefix[a.n]};
-  pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+  pipe_run<DType::U8, RedOp::COPY, 1, D>(lds, m, 1);
   // partial last tiles: one block each, bounded plain loads
   for (int k = blockIdx.x; k < a.ntail; k += gridDim.x) {
     const kern::CopyDesc& d = a.d[a.tail_idx[k]];
@@ -193,7 +194,9 @@ hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t
   return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, false);
 }
 
-hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream) {
+hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks, int depth) {
+  if (max_blocks <= 0) max_blocks = kK2Grid;
+  if (depth <= 0) depth = kK2Depth;
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   for (int base = 0; base < n; base += kMaxCopyDescs) {
     dev::CopyArgs a{};
@@ -217,8 +220,10 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream) {
     }
     if (a.n == 0) continue;
     a.prefix[a.n] = acc;
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), 256));
-    hipLaunchKernelGGL(dev::k2_multi_copy, dim3(grid), dim3(256), 0, stream, a);
+    const int grid =
+        (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), (uint64_t)max_blocks));
+    if (depth >= 8) hipLaunchKernelGGL(dev::k2_multi_copy<8>, dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(dev::k2_multi_copy<4>, dim3(grid), dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

@@ -69,9 +69,13 @@ def reduce_nway_reference(srcs: Sequence[torch.Tensor], op: str = "sum") -> torc
     return acc.to(dt)
 
 
-def multi_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
-    """K2: copy srcs[i] -> dsts[i] for every i in ONE kernel launch."""
-    _C().multi_copy(list(srcs), list(dsts))
+def multi_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor], max_blocks: int = 0,
+               depth: int = 0) -> None:
+    """K2: copy srcs[i] -> dsts[i] for every i in ONE kernel launch.
+
+    ``max_blocks`` caps the grid and ``depth`` (4 or 8) sets the LDS-DMA ring
+    depth; 0 keeps the tuned defaults (csrc/kernels/kernel_api.h kK2Grid/kK2Depth)."""
+    _C().multi_copy(list(srcs), list(dsts), max_blocks, depth)
 
 
 def _byte_view(t: torch.Tensor) -> torch.Tensor:

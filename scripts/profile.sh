@@ -6,8 +6,19 @@ REPO=$(pwd)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 cd /tmp
+if [ "${PDCC_PMC_ONLY:-0}" != 1 ]; then
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_kern" -o kb -- \
   python3 "$REPO/scripts/kernel_bench.py" > "$REPO/gpurun_out/prof_kern.log" 2>&1 || exit $?
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$REPO/gpurun_out/prof_ipc" -o ipc -- \
   python3 "$REPO/scripts/ipc_demo.py" > "$REPO/gpurun_out/prof_ipc.log" 2>&1 || exit $?
+fi
+if [ "${PDCC_PMC:-1}" = 1 ]; then
+  # hardware counters: one derived counter per run (FETCH_SIZE and WRITE_SIZE do
+  # not fit one pass on gfx950), kernel-trace only alongside --pmc
+  for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"; do
+    tag=$(echo $set | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -k 10 150 rocprofv3 --pmc $set --kernel-trace --output-format csv -d "$REPO/gpurun_out/pmc_$tag" \
+      -o pmc -- python3 "$REPO/scripts/pmc_k1.py" > "$REPO/gpurun_out/pmc_$tag.log" 2>&1 || exit $?
+  done
+fi
 echo profile-done
