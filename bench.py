@@ -25,6 +25,7 @@ import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +34,7 @@ sys.path.insert(0, ROOT)
 BASELINE_BUSBW = {2: 6.14, 4: 5.49, 8: 3.16}  # BASELINE.md §2.1 (reference stack, Gloo/CPU)
 SMALL = os.environ.get("PDCC_BENCH_SMALL", "0") == "1"  # functional rehearsal sizes for the extras
 NBYTES = 1 << 30
+EXTRAS_PARTIAL: dict = {}  # run_extras fills this in place (reported even if a deadline fires)
 
 
 def busbw(nbytes: int, n: int, sec: float) -> float:
@@ -126,15 +128,9 @@ def main():
     del y
 
     value = busbw(args.bytes, world, ms_per_step / 1e3)
-    extras = {}
-    if args.extras:
-        try:
-            extras = run_extras(world, rank, dev, native, x)
-        except Exception as e:  # extras never break the headline line
-            extras = {"error": f"{type(e).__name__}: {e}"[:500]}
 
-    if rank == 0:
-        line = {
+    def headline(extras):
+        return {
             "metric": "all_reduce busbw (GB/s) + p50 latency, 1 GiB fp32",
             "value": round(value, 3),
             "unit": "GB/s",
@@ -162,7 +158,34 @@ def main():
             "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
             "extras": extras,
         }
-        print(json.dumps(line), flush=True)
+
+    # The headline is already measured: whatever the extras do (a stuck peer on a
+    # new topology, say), the JSON line gets printed and the process exits.
+    printed = threading.Lock()
+
+    def emit(extras):
+        if rank == 0 and printed.acquire(blocking=False):
+            print(json.dumps(headline(extras)), flush=True)
+
+    def deadline(what):
+        emit({"error": f"{what} exceeded its deadline", "partial": dict(EXTRAS_PARTIAL)})
+        sys.stderr.flush()
+        os._exit(0)
+
+    extras = {}
+    if args.extras:
+        timer = threading.Timer(float(os.environ.get("PDCC_BENCH_EXTRAS_S", "300")), deadline, args=("extras",))
+        timer.daemon = True
+        timer.start()
+        try:
+            extras = run_extras(world, rank, dev, native, x)
+        except Exception as e:  # extras never break the headline line
+            extras = {"error": f"{type(e).__name__}: {e}"[:500]}
+        timer.cancel()
+    emit(extras)
+    guard = threading.Timer(60.0, lambda: os._exit(0))  # teardown must not hang the job either
+    guard.daemon = True
+    guard.start()
     dist.destroy_process_group()
 
 
@@ -188,7 +211,7 @@ def run_extras(world, rank, dev, native, x):
 
     from pytorch_distributed_collective_communication_amd import ops
 
-    out = {}
+    out = EXTRAS_PARTIAL  # filled in place, so a deadline still reports what finished
     # K1 on this GPU: 2-source fp32 reduce of 256 MiB per source, LDS-DMA vs register staging
     n = 64 << 20
     a = torch.rand(n, device=dev)
@@ -214,11 +237,14 @@ def run_extras(world, rank, dev, native, x):
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         return f.item() > 0
 
+    big = (1 << 30) if not SMALL else (64 << 20)
     for algo in ("rccl", "ipc"):
         try:
             gb.set_algo(algo)
             progress(f"algo A/B: {algo}")
-            for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, (1 << 30) if not SMALL else (64 << 20)):
+            for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, 256 << 20, big):
+                if nbytes == 256 << 20 and SMALL:
+                    continue
                 t = x[: nbytes // 4]
                 lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
                 out[f"allreduce_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
@@ -227,6 +253,29 @@ def run_extras(world, rank, dev, native, x):
             v = torch.full((1 << 20,), float(rank + 1), device=dev)
             dist.all_reduce(v, group=g)
             good = bool(torch.all(v == world * (world + 1) / 2).item())
+            # the other collectives at 1 MiB and the big size (S = total bytes, nccl-tests factors)
+            from pytorch_distributed_collective_communication_amd.utils import busbw as bb
+
+            for nbytes in (1 << 20, big):
+                per = nbytes // 4 // world
+                src = x[:per]
+                full = torch.empty(per * world, device=dev)
+                rs_out = torch.empty(per, device=dev)
+                cases = {
+                    "broadcast": ("broadcast", nbytes, lambda: dist.broadcast(x[: nbytes // 4], src=0, group=g)),
+                    "all_gather": ("all_gather", nbytes, lambda: dist.all_gather_into_tensor(full, src, group=g)),
+                    "reduce_scatter": ("reduce_scatter", nbytes,
+                                       lambda: dist.reduce_scatter_tensor(rs_out, x[: per * world], group=g)),
+                }
+                for name, (coll, total, fn) in cases.items():
+                    lat = _time_op(fn, 10 if nbytes >= (16 << 20) else 30)
+                    out[f"{name}_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
+                    out[f"{name}_{algo}_{nbytes}B_busbw"] = round(bb(coll, total, world, lat), 1)
+                ag_in = torch.full((per,), float(rank), device=dev)
+                dist.all_gather_into_tensor(full, ag_in, group=g)
+                good = good and bool(torch.equal(full.view(world, per)[:, 0].cpu(),
+                                                  torch.arange(world, dtype=torch.float32)))
+                del full, ag_in, rs_out
             out[f"allreduce_{algo}_correct"] = good
         except Exception as e:
             out[f"allreduce_{algo}_error"] = f"{type(e).__name__}: {e}"[:300]

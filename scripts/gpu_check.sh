@@ -24,6 +24,9 @@ for s in "$@"; do
         python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29534 bench.py --gpus 2 --steps 3 --warmup 1 --bytes 67108864 ;;
     kprof) step kprof 600 python scripts/kernel_bench.py ;;
+    benchdeadline) PDCC_BENCH_SMALL=1 PDCC_BENCH_EXTRAS_S=4 step benchdeadline 300 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 3 \
+        --warmup 1 --bytes 67108864 ;;
     profile) step profile 1500 bash scripts/profile.sh ;;
     pmc) PDCC_PMC_ONLY=1 step pmc 600 bash scripts/profile.sh ;;
     k2sweep) step k2sweep 300 python scripts/k2_sweep.py ;;
