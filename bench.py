@@ -128,6 +128,10 @@ def main():
     del y
 
     value = busbw(args.bytes, world, ms_per_step / 1e3)
+    try:  # the autotuner's decisions for the headline path (size bucket -> engine, times)
+        EXTRAS_PARTIAL["autotune"] = native.autotune_table()
+    except Exception:
+        pass
 
     def headline(extras):
         return {

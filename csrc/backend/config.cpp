@@ -59,6 +59,9 @@ Config Config::from_env() {
   c.ipc_copy_max = env_size("PDCC_IPC_COPY_MAX", c.ipc_copy_max);
   c.ipc_max_staging = env_size("PDCC_IPC_MAX_STAGING", c.ipc_max_staging);
   c.ipc_enable = env_bool("PDCC_IPC", c.ipc_enable);
+  c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
+  c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
+  c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
   c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
   if (const char* sm = env("PDCC_STREAM")) {
     std::string v(sm);

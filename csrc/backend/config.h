@@ -19,6 +19,12 @@ struct Config {
   size_t ipc_copy_max = 1u << 20;          // PDCC_IPC_COPY_MAX    broadcast/gather/... <= this: IPC
   size_t ipc_max_staging = 512u << 20;     // PDCC_IPC_MAX_STAGING per parity; larger messages are chunked
   bool ipc_enable = true;                  // PDCC_IPC=0 disables the peer-memory path
+  // Online autotuner (GPU all_reduce, groups where both RCCL and IPC are feasible): the first call
+  // in each power-of-two size bucket >= autotune_min runs both engines on scratch copies, checks
+  // that the IPC result matches RCCL's, times both and adopts the faster one on every rank.
+  bool autotune = true;                    // PDCC_AUTOTUNE=0 keeps the static thresholds above
+  size_t autotune_min = 64u << 10;         // PDCC_AUTOTUNE_MIN
+  size_t autotune_max = 4ull << 30;        // PDCC_AUTOTUNE_MAX (tuning clones the tensor twice)
   // PDCC_STREAM: auto (default) = synchronous collectives (async_op=False) on the caller's stream,
   // async ones on a normal-priority comm stream; high = auto with a high-priority comm stream;
   // comm = always the comm stream; current = always the caller's stream.

@@ -15,6 +15,7 @@
 
 #include <unistd.h>
 
+#include <cmath>
 #include <cstring>
 
 #include "../device/comm_util.h"
@@ -118,6 +119,24 @@ void multi_copy_or_memcpy(const std::vector<kern::CopyDesc>& d, hipStream_t s) {
     for (const auto& x : d)
       if (x.bytes) PDCC_HIP(hipMemcpyAsync(x.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, s));
   }
+}
+
+int size_bucket(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned long long)bytes) : 0; }
+
+// host path only competes for small messages, where its latency can beat a GPU protocol
+constexpr size_t kHostTuneMax = 4u << 20;
+
+// autotuner numerics check: candidate result vs the reference engine's result on the same data
+bool results_match(const at::Tensor& ref, const at::Tensor& got, RedOpType op, int world) {
+  if (!ref.is_floating_point() || op == RedOpType::MAX || op == RedOpType::MIN) return at::equal(ref, got);
+  const at::Tensor r = ref.to(at::kFloat), g = got.to(at::kFloat);
+  const bool wide = ref.scalar_type() == at::kFloat || ref.scalar_type() == at::kDouble;
+  // engines differ only in summation order (and, for 16-bit types, in where they round):
+  // allow a few ulps per rank relative to the largest magnitude; stale or misplaced data is far off
+  const double amax = r.abs().max().item<double>();
+  const double tol = (wide ? 4e-7 : 8e-3) * world;
+  if (!std::isfinite(amax)) return at::equal(ref, got);
+  return at::allclose(g, r, tol, tol * amax + 1e-30);
 }
 
 }  // namespace
@@ -335,8 +354,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
   ncclDataType_t nd;
   ncclRedOp_t no;
   const bool nok = nccl_dtype(t.scalar_type(), nd) && nccl_op(op, t.scalar_type(), no);
-  const Algo a = choose(cname, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
-  if (a == Algo::HOST) {
+  const Algo a0 = choose(cname, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
+  if (a0 == Algo::HOST) {
     at::Tensor h = t.cpu();
     if (rooted) shm().reduce(h.data_ptr(), h.numel(), h.scalar_type(), op, root, to);
     else shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
@@ -345,35 +364,157 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     return cpu_done(cname, {t});
   }
   at::Tensor w = prep_in(t);
+  Algo a2 = a0;
+  if (!rooted && !coalescing_) {
+    const auto cands = tune_candidates(cname, bytes, ds.rccl_ok && nok, ds.ipc_ok && kok);
+    if (!cands.empty()) {
+      a2 = tuned(cname, bytes);
+      if (a2 == Algo::AUTO) {
+        c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
+        const hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device).stream();
+        std::vector<at::Tensor> scratch;
+        for (size_t k = 0; k < cands.size(); ++k) scratch.push_back(w.clone(at::MemoryFormat::Contiguous));
+        a2 = autotune(
+            cname, bytes, ds, cands,
+            [&](size_t k) { enqueue_allreduce(cands[k], scratch[k], kd, ko, nd, no, op, root, false, ds, cs, to); },
+            [&](size_t r, size_t k) { return results_match(scratch[r], scratch[k], op, size_); });
+      }
+    }
+  }
+  const Algo a = a2;
+  if (a == Algo::HOST) {
+    // tuned to the host transport (small messages on groups without RCCL)
+    at::Tensor h = t.cpu();
+    shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
+    t.copy_(h);
+    record(cname, "host", bytes, t0);
+    return cpu_done(cname, {t});
+  }
   std::shared_ptr<IpcComm> icp;
   if (a == Algo::IPC) {
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
   auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = rooted ? (one_shot ? kern::IpcColl::REDUCE_1SHOT : kern::IpcColl::REDUCE_2SHOT)
-                      : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
-      c.dtype = kd;
-      c.op = ko;
-      c.root = root;
-      c.avg_div = size_;
-      c.bytes = bytes;
-      c.in[0] = w.data_ptr();
-      c.out[0] = w.data_ptr();
-      ipc_chunked(*icp, c, icp->max_staging(), s);
-    } else if (rooted) {
-      PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc->get(), s));
-    } else {
-      PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc->get(), s));
-    }
+    enqueue_allreduce(a, w, kd, ko, nd, no, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
   record(cname, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
   return work;
+}
+
+void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko,
+                                           ncclDataType_t nd, ncclRedOp_t no, RedOpType op, int root, bool rooted,
+                                           DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+  if (a == Algo::IPC) {
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    const bool one_shot = w.nbytes() <= cfg_.ipc_1shot_max;
+    c.coll = rooted ? (one_shot ? kern::IpcColl::REDUCE_1SHOT : kern::IpcColl::REDUCE_2SHOT)
+                    : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
+    c.dtype = kd;
+    c.op = ko;
+    c.root = root;
+    c.avg_div = size_;
+    c.bytes = w.nbytes();
+    c.in[0] = w.data_ptr();
+    c.out[0] = w.data_ptr();
+    ipc_chunked(ic, c, ic.max_staging(), s);
+  } else if (a == Algo::RCCL) {
+    RcclComm& rc = rccl(ds);
+    if (rooted) PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
+    else PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
+  } else {  // HOST, synchronous (autotuner candidate)
+    PDCC_HIP(hipStreamSynchronize(s));
+    at::Tensor h = w.cpu();
+    if (rooted) shm().reduce(h.data_ptr(), h.numel(), h.scalar_type(), op, root, to);
+    else shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
+    const_cast<at::Tensor&>(w).copy_(h);
+  }
+}
+
+// =================================================================== autotuner
+std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const {
+  std::vector<Algo> v;
+  if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || c != Coll::ALLREDUCE || !ipc_can || !same_host_) return v;
+  if (bytes < cfg_.autotune_min || bytes > cfg_.autotune_max) return v;
+  if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
+  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
+  else return {};
+  v.push_back(Algo::IPC);
+  return v;
+}
+
+Algo ProcessGroupMI355X::tuned(Coll c, size_t bytes) {
+  std::lock_guard<std::mutex> lk(tune_mu_);
+  auto it = tune_.find({(int)c, size_bucket(bytes)});
+  return it == tune_.end() ? Algo::AUTO : it->second.algo;
+}
+
+Algo ProcessGroupMI355X::autotune(Coll c, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
+                                  const std::function<void(size_t)>& run,
+                                  const std::function<bool(size_t, size_t)>& same) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
+  const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device).stream();
+  const size_t n = cands.size();
+  // 1) one run each on identical copies of the caller's data, then compare with the reference
+  for (size_t k = 0; k < n; ++k) run(k);
+  PDCC_HIP(hipStreamSynchronize(s));
+  std::vector<double> v(2 * n, 0.0);  // [time_us x n, mismatch x n], MAX-reduced across ranks
+  for (size_t k = 1; k < n; ++k) v[n + k] = same(0, k) ? 0.0 : 1.0;
+  // 2) time `iters` back-to-back runs of each engine with events on the caller's stream
+  const int iters = bytes >= (64u << 20) ? 3 : bytes >= (1u << 20) ? 10 : 30;
+  std::vector<hipEvent_t> ev(n + 1);
+  for (auto& e : ev) PDCC_HIP(hipEventCreate(&e));
+  PDCC_HIP(hipEventRecord(ev[0], s));
+  for (size_t k = 0; k < n; ++k) {
+    for (int i = 0; i < iters; ++i) run(k);
+    PDCC_HIP(hipEventRecord(ev[k + 1], s));
+  }
+  PDCC_HIP(hipEventSynchronize(ev[n]));
+  for (size_t k = 0; k < n; ++k) {
+    float ms = 0.f;
+    PDCC_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+    v[k] = 1e3 * ms / iters;
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  // 3) every rank adopts the same engine: slowest rank's time, any rank's mismatch
+  shm().allreduce(v.data(), v.size(), at::kDouble, RedOpType::MAX, timeout_);
+  size_t best = 0;
+  for (size_t k = 1; k < n; ++k)
+    if (v[n + k] == 0.0 && v[k] < v[best]) best = k;
+  TuneEntry te;
+  for (size_t k = 0; k < n; ++k) {
+    if (cands[k] == Algo::IPC) {
+      te.ipc_us = v[k];
+      te.valid = v[n + k] == 0.0;
+    } else {
+      te.rccl_us = v[k];  // the reference engine (RCCL, or the host transport without RCCL)
+    }
+  }
+  te.algo = cands[best];
+  {
+    std::lock_guard<std::mutex> lk(tune_mu_);
+    tune_[{(int)c, size_bucket(bytes)}] = te;
+  }
+  if (cfg_.log_level >= 1 && rank_ == 0)
+    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us%s -> %s\n", coll_name(c), bytes,
+            cands[0] == Algo::RCCL ? "rccl" : "host", te.rccl_us, te.ipc_us, te.valid ? "" : " (MISMATCH)",
+            te.algo == Algo::IPC ? "ipc" : (te.algo == Algo::RCCL ? "rccl" : "host"));
+  return te.algo;
+}
+
+std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table() {
+  std::lock_guard<std::mutex> lk(tune_mu_);
+  std::vector<TuneRecord> out;
+  for (const auto& kv : tune_) {
+    const TuneEntry& e = kv.second;
+    out.push_back({coll_name((Coll)kv.first.first), 1ull << kv.first.second, 2ull << kv.first.second, e.rccl_us,
+                   e.ipc_us, e.valid,
+                   e.algo == Algo::IPC ? "ipc" : (e.algo == Algo::RCCL ? "rccl" : "host")});
+  }
+  return out;
 }
 
 // =================================================================== broadcast

@@ -331,10 +331,40 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::vector<FrRecord> flight_recorder();
   std::string flight_recorder_dump(size_t last = 16);
 
+  // autotuner decisions so far: one row per (collective, power-of-two size bucket)
+  struct TuneRecord {
+    std::string coll;
+    uint64_t lo, hi;  // bucket [lo, hi) in bytes
+    double rccl_us, ipc_us;
+    bool valid;       // IPC result matched RCCL's on every rank
+    std::string algo;
+  };
+  std::vector<TuneRecord> autotune_table();
+
  private:
   std::vector<c10::intrusive_ptr<WorkMI355X>> coalesced_cpu_;
   int (*roctx_push_)(const char*) = nullptr;
   int (*roctx_pop_)() = nullptr;
+
+  // online autotuner (gpu_ops.cpp)
+  struct TuneEntry {
+    double rccl_us = 0, ipc_us = 0;
+    bool valid = false;
+    Algo algo = Algo::AUTO;
+  };
+  std::map<std::pair<int, int>, TuneEntry> tune_;  // (coll, floor(log2 bytes)) -> decision
+  std::mutex tune_mu_;
+  // engines worth timing for this call (reference engine first); empty = no tuning
+  std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const;
+  Algo tuned(Coll c, size_t bytes);
+  // run every candidate once on its own scratch copy via `run(k)`, check `same(0, k)` against
+  // the reference, time `iters` more runs each, agree across ranks (host transport), remember
+  // and return the winner
+  Algo autotune(Coll c, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
+                const std::function<void(size_t)>& run, const std::function<bool(size_t, size_t)>& same);
+  void enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko, ncclDataType_t nd,
+                         ncclRedOp_t no, c10d::ReduceOp::RedOpType op, int root, bool rooted, DeviceState& ds,
+                         hipStream_t s, std::chrono::milliseconds to);
 
   std::mutex stats_mu_;
   std::map<std::string, OpStats> stats_;

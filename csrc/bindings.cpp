@@ -111,6 +111,22 @@ PYBIND11_MODULE(_C, m) {
                d[py::str(kv.first)] = py::make_tuple(kv.second.calls, kv.second.bytes, kv.second.host_ms);
              return d;
            })
+      .def("autotune_table",
+           [](pdcc::ProcessGroupMI355X& pg) {
+             py::list l;
+             for (const auto& r : pg.autotune_table()) {
+               py::dict d;
+               d["coll"] = r.coll;
+               d["lo"] = r.lo;
+               d["hi"] = r.hi;
+               d["ref_us"] = r.rccl_us;
+               d["ipc_us"] = r.ipc_us;
+               d["ipc_valid"] = r.valid;
+               d["algo"] = r.algo;
+               l.append(d);
+             }
+             return l;
+           })
       .def("flight_recorder",
            [](pdcc::ProcessGroupMI355X& pg) {
              py::list l;

@@ -12,6 +12,8 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
 | PDCC_IPC_MAX_STAGING | 512M | staging bytes per parity; larger calls are chunked |
+| PDCC_AUTOTUNE | 1 | GPU all_reduce: time RCCL vs IPC on the first call per power-of-two size bucket (IPC result checked against RCCL's), adopt the faster on all ranks |
+| PDCC_AUTOTUNE_MIN / _MAX | 64K / 4G | size range the autotuner covers (outside: the static thresholds) |
 | PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
@@ -54,6 +56,9 @@ class Config:
     ipc_2shot_max: int = 8 << 20
     ipc_copy_max: int = 1 << 20
     ipc_max_staging: int = 512 << 20
+    autotune: bool = True
+    autotune_min: int = 64 << 10
+    autotune_max: int = 4 << 30
     world1_local: bool = True
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
@@ -71,7 +76,8 @@ class Config:
 _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
-    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "world1_local": "PDCC_WORLD1_LOCAL",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "autotune": "PDCC_AUTOTUNE",
+    "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
     "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
     "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",

@@ -125,3 +125,10 @@ def last_algo(group=None) -> str:
 
 def describe(group=None) -> str:
     return native_backend(group).describe()
+
+
+def autotune_table(group=None) -> list:
+    """Decisions of the online autotuner so far (one dict per collective and
+    power-of-two size bucket: reference-engine and IPC times, whether the IPC
+    result matched, and the adopted engine). See PDCC_AUTOTUNE in config.py."""
+    return native_backend(group).autotune_table()

@@ -417,3 +417,25 @@ def async_ordering(rank, size, device="cuda", rounds=20):
     for k, t in enumerate(xs):
         ok.append(bool(torch.all(t == sum(k + r for r in range(size))).item()))
     return ok
+
+
+def autotune_probe(rank, size, device="cuda"):
+    """all_reduce across the autotuner's size buckets: the first call of each
+    bucket times both engines on scratch copies; every call must still return
+    the right sum, and the decision table must be identical on all ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    ok = []
+    for dt in (torch.float32, torch.bfloat16):
+        for n in (16 << 10, 1 << 18, 1 << 20, 4 << 20):
+            x = (torch.arange(n, device=d) % 13).to(dt) + rank
+            exp = ((torch.arange(n, device=d) % 13).float() * size + size * (size - 1) / 2)
+            for _ in range(3):
+                y = x.clone()
+                dist.all_reduce(y)
+                ok.append(bool(torch.allclose(y.float(), exp, rtol=1e-2 if dt == torch.bfloat16 else 0)))
+    return {"ok": ok, "table": be.autotune_table()}

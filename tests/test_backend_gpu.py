@@ -107,3 +107,17 @@ def test_async_ops_stream_ordering(world, stream):
         env["PDCC_ALGO"] = "ipc"
     for ok in _gpu_launch(W.async_ordering, world, env=env):
         assert all(ok), ok
+
+
+def test_autotuner_shared_gpu():
+    # ranks share one GPU, so RCCL is out: the tuner weighs IPC against the host
+    # transport for buckets <= 4 MiB and leaves 16 MiB to the static choice
+    res = _gpu_launch(W.autotune_probe, 2, env={"PDCC_LOG_LEVEL": "1"})
+    for r in res:
+        assert all(r["ok"]), r["ok"]
+    assert res[0]["table"] == res[1]["table"]
+    los = sorted(e["lo"] for e in res[0]["table"])
+    assert los == [64 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20], res[0]["table"]
+    for e in res[0]["table"]:
+        assert e["coll"] == "allreduce" and e["ipc_valid"], e
+        assert e["algo"] in ("ipc", "host")
