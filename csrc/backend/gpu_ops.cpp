@@ -227,8 +227,10 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
 }
 
 void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per_call_max, hipStream_t s) {
-  size_t chunk = per_call_max / kern::kTileBytes * kern::kTileBytes;
-  if (chunk == 0) chunk = kern::kTileBytes;
+  // whole rows of `size_` tiles per chunk: 2-shot staging is sized to whole rows
+  const size_t row = (size_t)size_ * kern::kTileBytes;
+  size_t chunk = per_call_max / row * row;
+  if (chunk == 0) chunk = row;
   const size_t total = call.bytes;
   if (total <= chunk) {
     ic.launch(call, s);

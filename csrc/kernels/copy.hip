@@ -63,10 +63,11 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 }
 
 // ----------------------------------------------------------- IPC copy family
+template <int W>
 __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
-  const int me = v.rank, W = v.world;
+  const int me = v.rank;
   const uint32_t ph0 = v.seq * 2u, ph1 = v.seq * 2u + 1u;
   char* mine = v.buf[me];
   const size_t nt = pad_tiles(c.bytes) / kTile;
@@ -95,9 +96,8 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       }
       block_barrier(v, ph1);
       if (me == c.root) return;
-      for (int j = 0; j < W; ++j) {  // phase 2: every owner's tiles, over all links at once
-        const int q = (me + j) % W;
-        const OneSrcMap m{v.buf[q], (char*)c.out[0], c.bytes, q + W * b, W * G, nt};
+      {  // phase 2: every owner's tiles, owners interleaved (all links at once)
+        const OwnerRowMap<W> m{&v, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -107,9 +107,8 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       if (c.coll == IpcColl::GATHER && me != c.root) return;
-      for (int j = 0; j < W; ++j) {
-        const int q = (me + j) % W;
-        const OneSrcMap m{v.buf[q], (char*)c.out[q], c.bytes, b, G, nt};
+      {
+        const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(me + b), b, G, nt};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -125,9 +124,8 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
     case IpcColl::ALLTOALL: {
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
-      for (int j = 0; j < W; ++j) {
-        const int q = (me + j) % W;
-        const OneSrcMap m{v.buf[q] + me * cpad, (char*)c.out[q], c.bytes, b, G, nt};
+      {
+        const PeerTileMap<W> m{&v, &c, me * cpad, c.bytes, (uint32_t)(me + b), b, G, nt};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -241,6 +239,13 @@ size_t ipc_staging_bytes(const IpcCall& c, int world) {
       return cpad * world;
     case IpcColl::BARRIER:
       return 0;
+    case IpcColl::ALLREDUCE_2SHOT:
+    case IpcColl::REDUCE_2SHOT:
+    case IpcColl::BROADCAST_2SHOT: {
+      // whole rows of W tiles: phase 2 (dev::OwnerRowMap) reads a partial last row's padding
+      const size_t row = (size_t)world * kTileBytes;
+      return (cpad + row - 1) / row * row;
+    }
     default:
       return cpad;
   }
@@ -273,7 +278,13 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
                         c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
                         c.coll == IpcColl::REDUCE_SCATTER;
   if (!reducing) {
-    hipLaunchKernelGGL(dev::k_ipc_copy, dim3(grid), dim3(256), 0, stream, v, c);
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL(dev::k_ipc_copy<WW>, dim3(grid), dim3(256), 0, stream, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   if (!supports(c.dtype, c.op)) return hipErrorInvalidValue;

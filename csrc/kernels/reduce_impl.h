@@ -127,6 +127,76 @@ struct OneSrcMap {  // copy tile t from one buffer to another
 
 constexpr int kCopyDepth = 4;
 
+// Owner-interleaved maps. A block's pipeline keeps DEPTH tiles in flight; if all
+// of them (and, with blocks in lockstep, all blocks of the rank) pull from the
+// same peer, a rank drives ONE xGMI link at a time. These maps rotate the owner
+// per item, per row and per block, so in-flight tiles spread over every peer.
+
+// 2-shot phase 2: tiles q + W*r of rows r = first + stride*k (owner q = rank whose
+// staging holds the reduced tile). A partial last row reads staging padding
+// (staging is sized to whole rows, see kern::ipc_staging_bytes); valid() = 0 there.
+template <int W>
+struct OwnerRowMap {
+  const IpcView* v;
+  char* d;
+  size_t dlim;
+  uint32_t rot;
+  size_t first, stride, nrows;
+  __device__ size_t count() const { return first < nrows ? ((nrows - 1 - first) / stride + 1) * W : 0; }
+  __device__ size_t tile(size_t i, int& q) const {
+    const uint32_t k = (uint32_t)i / W, j = (uint32_t)i - k * W;
+    q = (int)((rot + j + k) % W);
+    return (size_t)q + (size_t)W * (first + stride * k);
+  }
+  __device__ const char* src(int, size_t i) const {
+    int q;
+    const size_t t = tile(i, q);
+    return v->buf[q] + t * kTile;
+  }
+  __device__ char* dst(size_t i) const {
+    int q;
+    return d + tile(i, q) * kTile;
+  }
+  __device__ size_t valid(size_t i) const {
+    int q;
+    const size_t o = tile(i, q) * kTile;
+    return o >= dlim ? 0 : (dlim - o < (size_t)kTile ? dlim - o : (size_t)kTile);
+  }
+};
+
+// all-gather / gather / all-to-all: (tile t of this block, source rank q) pairs;
+// source q's tile lives at v->buf[q] + sbase + t*kTile and lands in out[q].
+template <int W>
+struct PeerTileMap {
+  const IpcView* v;
+  const IpcCall* c;
+  size_t sbase;
+  size_t dlim;
+  uint32_t rot;
+  size_t first, stride, ntiles;
+  __device__ size_t count() const { return first < ntiles ? ((ntiles - 1 - first) / stride + 1) * W : 0; }
+  __device__ size_t tile(size_t i, int& q) const {
+    const uint32_t k = (uint32_t)i / W, j = (uint32_t)i - k * W;
+    q = (int)((rot + j + k) % W);
+    return first + stride * k;
+  }
+  __device__ const char* src(int, size_t i) const {
+    int q;
+    const size_t t = tile(i, q);
+    return v->buf[q] + sbase + t * kTile;
+  }
+  __device__ char* dst(size_t i) const {
+    int q;
+    const size_t t = tile(i, q);
+    return (char*)c->out[q] + t * kTile;
+  }
+  __device__ size_t valid(size_t i) const {
+    int q;
+    const size_t o = tile(i, q) * kTile;
+    return o >= dlim ? 0 : (dlim - o < (size_t)kTile ? dlim - o : (size_t)kTile);
+  }
+};
+
 template <DType DT, RedOp OP, int W>
 __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   constexpr int D = DepthFor<W>::value;
@@ -159,10 +229,9 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       }
       block_barrier(v, ph1);
       if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
-      // phase 2: pull every owner's reduced tiles (rotated start balances links)
-      for (int j = 0; j < W; ++j) {
-        const int q = (me + j) % W;
-        const OneSrcMap m{v.buf[q], (char*)c.out[0], c.bytes, q + W * b, W * G, nt};
+      // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
+      {
+        const OwnerRowMap<W> m{&v, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;

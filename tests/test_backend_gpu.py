@@ -54,11 +54,12 @@ def test_shared_gpu_ipc_op_matrix():
                 assert val == pytest.approx(exp), key
 
 
-@pytest.mark.parametrize("oneshot_max", ["512K", "0"])
-def test_shared_gpu_ipc_bulk(oneshot_max):
-    # small staging forces the chunked path; 1SHOT_MAX=0 forces 2-shot everywhere
+@pytest.mark.parametrize("world,oneshot_max", [(2, "512K"), (2, "0"), (3, "0")])
+def test_shared_gpu_ipc_bulk(world, oneshot_max):
+    # small staging forces the chunked path; 1SHOT_MAX=0 forces 2-shot everywhere;
+    # world 3 exercises rows of 3 tiles with a partial last row in every chunk
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": oneshot_max, "PDCC_IPC_MAX_STAGING": "2M"}
-    for ok in _gpu_launch(W.large, 2, env=env):
+    for ok in _gpu_launch(W.large, world, env=env):
         assert all(ok.values()), ok
 
 
