@@ -439,3 +439,35 @@ def autotune_probe(rank, size, device="cuda"):
                 dist.all_reduce(y)
                 ok.append(bool(torch.allclose(y.float(), exp, rtol=1e-2 if dt == torch.bfloat16 else 0)))
     return {"ok": ok, "table": be.autotune_table()}
+
+
+def gpu_fault_victim(rank, size, q, group_timeout_s=4):
+    """Two ranks on the IPC path; rank 1 dies after setup. Rank 0's next GPU
+    all_reduce spins in the cross-GPU barrier until the group timeout (bounded
+    spin, error word), the watchdog poisons the group, and rank 0 gets a
+    RuntimeError instead of a hang."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import init_process
+
+    def body(r, s):
+        x = torch.ones(1 << 16, device="cuda")
+        dist.all_reduce(x)  # IPC staging + peer mappings set up on both ranks
+        torch.cuda.synchronize()
+        dist.barrier()
+        if r == 1:
+            os._exit(13)
+        time.sleep(0.5)
+        t0 = time.time()
+        try:
+            for _ in range(3):
+                dist.all_reduce(x)
+                torch.cuda.synchronize()
+                time.sleep(0.3)
+            return ("no error", time.time() - t0)
+        except RuntimeError as e:
+            return (str(e), time.time() - t0)
+
+    res = init_process(rank, size, body, bind_device=True, timeout_s=group_timeout_s)
+    q.put((rank, res))

@@ -122,3 +122,31 @@ def test_autotuner_shared_gpu():
     for e in res[0]["table"]:
         assert e["coll"] == "allreduce" and e["ipc_valid"], e
         assert e["algo"] in ("ipc", "host")
+
+
+def test_gpu_peer_death_is_detected():
+    import os
+
+    import torch.multiprocessing as mp
+
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import free_port
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    os.environ["MASTER_PORT"] = str(free_port())
+    os.environ["PDCC_ALGO"] = "ipc"
+    try:
+        ps = [ctx.Process(target=W.gpu_fault_victim, args=(r, 2, q)) for r in range(2)]
+        for p in ps:
+            p.start()
+        rank, (msg, elapsed) = q.get(timeout=180)
+    finally:
+        os.environ.pop("PDCC_ALGO", None)
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    assert rank == 0
+    assert "IPC" in msg or "error state" in msg or "timed out" in msg, msg
+    assert elapsed < 30, elapsed
+    assert ps[1].exitcode == 13
