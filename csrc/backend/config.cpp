@@ -59,6 +59,8 @@ Config Config::from_env() {
   c.ipc_copy_max = env_size("PDCC_IPC_COPY_MAX", c.ipc_copy_max);
   c.ipc_max_staging = env_size("PDCC_IPC_MAX_STAGING", c.ipc_max_staging);
   c.ipc_enable = env_bool("PDCC_IPC", c.ipc_enable);
+  c.ipc_selftest = env_bool("PDCC_IPC_SELFTEST", c.ipc_selftest);
+  c.ipc_selftest_ms = env_int("PDCC_IPC_SELFTEST_MS", c.ipc_selftest_ms);
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
   c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
@@ -85,7 +87,8 @@ Config Config::from_env() {
 
 std::string Config::describe() const {
   std::ostringstream o;
-  o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_1shot_max=" << ipc_1shot_max
+  o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_selftest=" << ipc_selftest
+    << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait

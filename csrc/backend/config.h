@@ -19,6 +19,12 @@ struct Config {
   size_t ipc_copy_max = 1u << 20;          // PDCC_IPC_COPY_MAX    broadcast/gather/... <= this: IPC
   size_t ipc_max_staging = 512u << 20;     // PDCC_IPC_MAX_STAGING per parity; larger messages are chunked
   bool ipc_enable = true;                  // PDCC_IPC=0 disables the peer-memory path
+  // Before a group first uses a device, every rank runs the IPC protocol once on known data (1-shot
+  // and 2-shot all-reduce, all-gather) with a short spin timeout and checks the results; one failure
+  // on any rank (handle open error, timeout, wrong data) disables IPC for the whole group, so a
+  // topology the protocol does not work on falls back to RCCL instead of hanging or corrupting data.
+  bool ipc_selftest = true;                // PDCC_IPC_SELFTEST
+  int ipc_selftest_ms = 20000;             // PDCC_IPC_SELFTEST_MS spin timeout during the self-test
   // Online autotuner (GPU all_reduce, groups where both RCCL and IPC are feasible): the first call
   // in each power-of-two size bucket >= autotune_min runs both engines on scratch copies, checks
   // that the IPC result matches RCCL's, times both and adopts the faster one on every rank.

@@ -123,6 +123,15 @@ void multi_copy_or_memcpy(const std::vector<kern::CopyDesc>& d, hipStream_t s) {
 
 int size_bucket(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned long long)bytes) : 0; }
 
+// is `s` being captured into a graph (torch.cuda.graph / parallel.graphs)?
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+bool capturing_on(int device) {
+  return capturing(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device).stream());
+}
+
 // host path only competes for small messages, where its latency can beat a GPU protocol
 constexpr size_t kHostTuneMax = 4u << 20;
 
@@ -183,7 +192,7 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   ds->device = d;
   ds->shared_device = shared;
   ds->rccl_ok = !shared;
-  ds->ipc_ok = ok;
+  ds->ipc_ok = ok && (!cfg_.ipc_selftest || ipc_selftest(*ds));
   if (cfg_.log_level >= 1)
     fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d shared_device=%d\n", rank_, d, bus,
             (int)ds->rccl_ok, (int)ds->ipc_ok, (int)shared);
@@ -211,19 +220,110 @@ IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
   return *ds.ipc;
 }
 
-Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can) {
-  (void)ds;
-  if (cfg_.force_algo == Algo::HOST) return Algo::HOST;
-  if (cfg_.force_algo == Algo::RCCL && rccl_can) return Algo::RCCL;
-  if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
-  if (ipc_can) {
-    size_t lim = cfg_.ipc_copy_max;
-    if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
-    if (bytes <= lim) return Algo::IPC;
+// PDCC_IPC_SELFTEST (default on): before a group's first GPU collective, every
+// rank runs the IPC protocol once on known data -- 1-shot all-reduce, 2-shot
+// all-reduce over rows of W tiles with a partial last row and a ragged tail, and
+// an all-gather -- with a short spin timeout. Two store votes decide (after the
+// communicator is built, after the checks): one failure on any rank (handle
+// export or mapping, spin timeout, wrong data) turns IPC off for the whole group,
+// so a topology the protocol does not work on falls back to RCCL (or the host
+// path) instead of hanging or corrupting data. Called from dev_state() with
+// init_mu_ held, on the group's comm stream (never a capturing one).
+bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
+  auto vote = [&](const std::string& key, bool mine) {
+    const auto v = store_allgather(store_, key, rank_, size_, std::vector<uint8_t>{(uint8_t)mine});
+    bool all = true;
+    for (const auto& x : v) all = all && !x.empty() && x[0] == 1;
+    return all;
+  };
+  const int64_t spin_ms = std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_selftest_ms, timeout_.count()));
+  std::string why;
+  bool ok = true;
+  try {
+    ds.ipc = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging,
+                                       (uint64_t)spin_ms, ds.shared_device);
+  } catch (const std::exception& e) {
+    ok = false;
+    why = e.what();
   }
-  if (rccl_can) return Algo::RCCL;
-  if (ipc_can) return Algo::IPC;
-  return Algo::HOST;
+  bool all = vote("pdcc/ipc_selftest/built", ok);
+  if (all) {
+    try {
+      IpcComm& ic = *ds.ipc;
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
+      const hipStream_t s = ds.stream.stream();
+      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+      const double tri = size_ * (size_ + 1) / 2.0;
+      for (const int64_t n : {int64_t{1000}, int64_t{3} * size_ * 1024 + 257}) {
+        const at::Tensor base = at::arange(n, opt).remainder(7);
+        at::Tensor x = base + (double)(rank_ + 1);
+        kern::IpcCall c{};
+        c.coll = n == 1000 ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT;
+        c.dtype = kern::DType::F32;
+        c.op = kern::RedOp::SUM;
+        c.avg_div = size_;
+        c.bytes = x.nbytes();
+        c.in[0] = x.data_ptr();
+        c.out[0] = x.data_ptr();
+        ic.launch(c, s);
+        ok = at::equal(x, base * (double)size_ + tri) && ok;
+      }
+      const int64_t m = 780;  // 3120 B per rank: whole 16-B vectors, one partial tile
+      const at::Tensor in = at::full({m}, (double)rank_, opt);
+      at::Tensor out = at::full({m * size_}, -1.0, opt);
+      kern::IpcCall c{};
+      c.coll = kern::IpcColl::ALLGATHER;
+      c.dtype = kern::DType::U8;
+      c.op = kern::RedOp::COPY;
+      c.bytes = in.nbytes();
+      c.in[0] = in.data_ptr();
+      for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
+      ic.launch(c, s);
+      ok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && ok;
+      if (ic.error_word() != 0) {
+        ok = false;
+        why = "a cross-GPU barrier timed out";
+      } else if (!ok) {
+        why = "wrong data";
+      }
+    } catch (const std::exception& e) {
+      ok = false;
+      why = e.what();
+    }
+    if (const char* f = std::getenv("PDCC_IPC_SELFTEST_FAIL"))  // test hook: this rank reports a failure
+      if (*f && std::atoi(f) == rank_) {
+        ok = false;
+        why = "PDCC_IPC_SELFTEST_FAIL";
+      }
+    all = vote("pdcc/ipc_selftest/result", ok);
+  }
+  if (!all) {
+    fprintf(stderr, "[pdcc r%d] IPC self-test failed (%s): group '%s' runs without the peer-memory path\n", rank_,
+            ok ? "on another rank" : why.c_str(), group_name_.c_str());
+    ds.ipc.reset();  // every rank voted after its own kernels finished: nothing touches these buffers any more
+    return false;
+  }
+  ds.ipc->set_timeout_ms((uint64_t)timeout_.count());
+  return true;
+}
+
+Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can) {
+  const Algo a = [&] {
+    if (cfg_.force_algo == Algo::HOST) return Algo::HOST;
+    if (cfg_.force_algo == Algo::RCCL && rccl_can) return Algo::RCCL;
+    if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
+    if (ipc_can) {
+      size_t lim = cfg_.ipc_copy_max;
+      if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
+      if (bytes <= lim) return Algo::IPC;
+    }
+    if (rccl_can) return Algo::RCCL;
+    if (ipc_can) return Algo::IPC;
+    return Algo::HOST;
+  }();
+  TORCH_CHECK(a != Algo::HOST || !capturing_on(ds.device), "pdcc: this ", coll_name(c), " (", bytes,
+              " B) would run on the host-staged engine, which cannot be captured into a graph");
+  return a;
 }
 
 void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per_call_max, hipStream_t s) {
@@ -257,7 +357,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
   // synchronous collectives (and PDCC_STREAM=current) run on the caller's stream: no
   // cross-stream event hand-off, which costs far more than the launch on this runtime
-  const bool on_current = cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_);
+  // (and graph capture always: the capturing stream is the only one the graph sees)
+  const bool cap = capturing(cur.stream());
+  const bool on_current = cap || cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_);
   const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : ds.stream;
   StreamSync& sy = *ds.sync;
   bool use_sig = false;
@@ -292,6 +394,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
     fn(comm.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
+  // graph capture: the graph node is the completion -- no event, nothing for the watchdog
+  if (cap) return cpu_done(c, std::move(outputs));
   if (comm != cur) {  // the caching allocator must not recycle these before the comm stream is done
     for (const auto& t : keep_alive)
       if (t.defined() && t.is_cuda())
@@ -371,6 +475,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     const auto cands = tune_candidates(cname, bytes, ds.rccl_ok && nok, ds.ipc_ok && kok);
     if (!cands.empty()) {
       a2 = tuned(cname, bytes);
+      const bool cap = capturing_on(ds.device);
+      if (a2 == Algo::AUTO && cap) a2 = a0;         // no timing runs inside a graph capture: static choice
+      if (a2 == Algo::HOST && cap) a2 = Algo::IPC;  // tuned to the host engine, which cannot be captured
       if (a2 == Algo::AUTO) {
         c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
         const hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device).stream();
@@ -877,6 +984,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
   const auto t0 = std::chrono::steady_clock::now();
   const Coll cname = is_send ? Coll::SEND : Coll::RECV;
   if (!ds.rccl_ok || cfg_.force_algo == Algo::HOST) {
+    TORCH_CHECK(!capturing_on(ds.device), "pdcc: ", is_send ? "send" : "recv",
+                " runs on the host transport here, which cannot be captured into a graph");
     // shared-device setups: through the host transport, synchronously
     if (is_send) {
       at::Tensor h = t.cpu().contiguous();

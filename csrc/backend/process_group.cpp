@@ -533,6 +533,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::cpu_done(Coll c, std::vector<
 
 // =================================================================== watchdog
 void ProcessGroupMI355X::watchdog_loop() {
+  // the caller's thread may capture collectives into a hipGraph while this one
+  // polls events: relaxed capture mode keeps those queries from breaking the capture
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
   while (!wd_stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(cfg_.watchdog_ms));
     std::vector<c10::intrusive_ptr<WorkMI355X>> live;

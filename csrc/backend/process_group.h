@@ -241,6 +241,8 @@ class ProcessGroupMI355X : public c10d::Backend {
   DeviceState& dev_state(const at::Tensor& t);
   RcclComm& rccl(DeviceState& ds);
   IpcComm& ipc(DeviceState& ds);
+  // PDCC_IPC_SELFTEST: run the IPC protocol once on known data; false = IPC off for this group
+  bool ipc_selftest(DeviceState& ds);
   Algo choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can);
   void before_op(Coll c, const std::vector<at::Tensor>& ts, int root);
   void debug_check(Coll c, const std::vector<at::Tensor>& ts, int root);

@@ -56,6 +56,15 @@ struct DeviceScope {
   ~DeviceScope() { hipSetDevice(prev); }
 };
 
+// An empty blob in the store means "this rank could not export": every rank
+// checks all blobs before opening any, so the whole group fails the same step
+// instead of some ranks waiting on the store for a handle that never comes.
+void check_blobs(const std::vector<std::vector<uint8_t>>& all, int self, const char* what) {
+  for (size_t r = 0; r < all.size(); ++r)
+    if ((int)r != self && all[r].empty())
+      throw std::runtime_error("pdcc: rank " + std::to_string(r) + " could not export its IPC " + what);
+}
+
 }  // namespace
 
 IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world,
@@ -71,15 +80,24 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
   DeviceScope ds(device);
-  const size_t sig = granule(kern::ipc_signal_bytes());
-  PDCC_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&my_flags_), sig, hipDeviceMallocUncached));
-  PDCC_HIP(hipMemset(my_flags_, 0, sig));
-  PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
-  *err_host_ = 0;
-  PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
-  PDCC_HIP(hipDeviceSynchronize());
-
-  const auto all = store_allgather(store_, key_ + "/ipc_sig", rank_, world_, handle_bytes(my_flags_));
+  std::vector<uint8_t> mine;
+  std::string err;
+  try {
+    const size_t sig = granule(kern::ipc_signal_bytes());
+    PDCC_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&my_flags_), sig, hipDeviceMallocUncached));
+    PDCC_HIP(hipMemset(my_flags_, 0, sig));
+    PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
+    *err_host_ = 0;
+    PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
+    PDCC_HIP(hipDeviceSynchronize());
+    mine = handle_bytes(my_flags_);
+  } catch (const std::exception& e) {
+    err = e.what();
+    mine.clear();  // published empty: the peers fail this step with us
+  }
+  const auto all = store_allgather(store_, key_ + "/ipc_sig", rank_, world_, mine);
+  if (!err.empty()) throw std::runtime_error(err);
+  check_blobs(all, rank_, "signal area");
   peer_flags_.assign(world_, nullptr);
   flags_maps_.assign(world_, nullptr);
   for (int r = 0; r < world_; ++r) {
@@ -96,7 +114,14 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
 IpcComm::~IpcComm() {
   try {
     DeviceScope ds(device_);
+    graph_mode_ = false;  // the group is gone: staging retired for captured graphs goes too
     unmap_staging();
+    for (auto& r : retired_) {
+      for (void* m : r.maps)
+        if (m) hipIpcCloseMemHandle(m);
+      if (r.mine) hipFree(r.mine);
+    }
+    retired_.clear();
     for (void* m : flags_maps_)
       if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
@@ -106,20 +131,40 @@ IpcComm::~IpcComm() {
 }
 
 void IpcComm::unmap_staging() {
-  for (void* m : staging_maps_)
-    if (m) hipIpcCloseMemHandle(m);
+  if (graph_mode_) {
+    // a captured graph has these buffers baked into its kernel arguments: keep them alive
+    if (my_staging_) retired_.push_back({my_staging_, staging_maps_});
+  } else {
+    for (void* m : staging_maps_)
+      if (m) hipIpcCloseMemHandle(m);
+    if (my_staging_) hipFree(my_staging_);
+  }
   staging_maps_.clear();
   peer_staging_.clear();
-  if (my_staging_) hipFree(my_staging_);
   my_staging_ = nullptr;
   cap_ = 0;
 }
 
 void IpcComm::map_staging(size_t cap) {
-  PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&my_staging_), granule(2 * cap)));
+  std::vector<uint8_t> mine;
+  std::string err;
+  try {
+    PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&my_staging_), granule(2 * cap)));
+    mine = handle_bytes(my_staging_);
+  } catch (const std::exception& e) {
+    err = e.what();
+    mine.clear();
+  }
+  const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_, mine);
+  try {
+    if (!err.empty()) throw std::runtime_error(err);
+    check_blobs(all, rank_, "staging buffer");
+  } catch (...) {
+    if (my_staging_) hipFree(my_staging_);  // nobody opened it: every rank stops before opening
+    my_staging_ = nullptr;
+    throw;
+  }
   cap_ = cap;
-  const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_,
-                                   handle_bytes(my_staging_));
   peer_staging_.assign(world_, nullptr);
   staging_maps_.assign(world_, nullptr);
   for (int r = 0; r < world_; ++r) {
@@ -149,19 +194,34 @@ void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
 }
 
 void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  PDCC_HIP(hipStreamIsCapturing(stream, &cs));
+  const bool capturing = cs != hipStreamCaptureStatusNone;
   const size_t need = kern::ipc_staging_bytes(call, world_);
-  if (need > 0) ensure_staging(need, stream);
+  if (need > 0) {
+    if (capturing && (need + kern::kTileBytes - 1) / kern::kTileBytes * kern::kTileBytes > cap_)
+      throw std::runtime_error(
+          "pdcc: this IPC collective needs more staging than the group has, and staging cannot grow while the "
+          "stream is being captured into a graph: run the collective once before capturing it "
+          "(parallel.graphs.capture does)");
+    ensure_staging(need, stream);
+  }
+  // Once a launch is captured, sequence numbers live on the device for good: a
+  // graph replays its kernel arguments verbatim, so the host count would go stale.
+  if (capturing) graph_mode_ = true;
   kern::IpcView v{};
   ++seq_;  // flags compare with a wrap-safe signed difference, so uint32 wrap is harmless
-  const size_t parity = seq_ & 1u;
   for (int r = 0; r < world_; ++r) {
-    v.buf[r] = peer_staging_.empty() ? nullptr : peer_staging_[r] + parity * cap_;
+    v.buf[r] = peer_staging_.empty() ? nullptr : peer_staging_[r];  // parity 0; the kernel adds cap for parity 1
     v.flags[r] = peer_flags_[r];
   }
   v.err = err_dev_;
+  v.seq_dev = my_flags_;
+  v.cap = cap_;
   v.rank = rank_;
   v.world = world_;
   v.seq = seq_;
+  v.dev_seq = graph_mode_ ? 1u : 0u;
   v.timeout_ticks = timeout_ticks_;
   if (shared_device_) {
     // all ranks' grids must be co-resident on ONE device (test setups): stay well

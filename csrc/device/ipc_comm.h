@@ -9,6 +9,10 @@
 // Consecutive calls alternate parity, which makes an end-of-call barrier
 // unnecessary: before a rank writes a parity again, the start barrier of the
 // call in between proves every peer has finished the call that last read it.
+//
+// Launches may be captured into a hipGraph (parallel/graphs.py): from the first
+// captured launch on, the kernels take their sequence number from a counter in
+// the own signal area, and staging a graph may reference is retired, not freed.
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <torch/csrc/distributed/c10d/Store.hpp>
@@ -34,8 +38,14 @@ class IpcComm {
   void ensure_staging(size_t bytes, hipStream_t stream);
   size_t max_staging() const { return max_staging_; }
 
-  // Launch one collective call (consumes one sequence number).
+  // Launch one collective call (consumes one sequence number). May be captured
+  // into a hipGraph once the staging is large enough for the call.
   void launch(kern::IpcCall call, hipStream_t stream);
+
+  // spin timeout of the cross-GPU barriers of later launches
+  void set_timeout_ms(uint64_t ms) { timeout_ticks_ = ms * 100000ull; }
+  // a launch was captured into a graph: sequence numbers live on the device from now on
+  bool graph_mode() const { return graph_mode_; }
 
   // Error word written by a kernel whose spin timed out (0 = healthy).
   uint32_t error_word() const;
@@ -67,6 +77,12 @@ class IpcComm {
   std::vector<void*> staging_maps_;
   int staging_gen_ = 0;
   uint32_t seq_ = 0;
+  bool graph_mode_ = false;
+  struct Retired {
+    char* mine;
+    std::vector<void*> maps;
+  };
+  std::vector<Retired> retired_;  // staging a captured graph may still use (freed with the group)
 };
 
 }  // namespace pdcc

@@ -68,8 +68,10 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t ph0 = v.seq * 2u, ph1 = v.seq * 2u + 1u;
-  char* mine = v.buf[me];
+  const uint32_t seq = call_seq(v);
+  const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
+  const size_t poff = (seq & 1u) ? v.cap : 0;
+  char* mine = v.buf[me] + poff;
   const size_t nt = pad_tiles(c.bytes) / kTile;
   const size_t cpad = nt * kTile;
 
@@ -81,7 +83,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       if (me == c.root) stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       if (me == c.root) return;
-      const OneSrcMap m{v.buf[c.root], (char*)c.out[0], c.bytes, b, G, nt};
+      const OneSrcMap m{v.buf[c.root] + poff, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
@@ -91,13 +93,13 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
         for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[0], mine, c.bytes, q + W * b, W * G, nt);
       block_barrier(v, ph0);
       if (me != c.root) {  // phase 1: fetch my owned tiles from the root (one link each)
-        const OneSrcMap m{v.buf[c.root], mine, cpad, me + W * b, W * G, nt};
+        const OneSrcMap m{v.buf[c.root] + poff, mine, cpad, me + W * b, W * G, nt};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       block_barrier(v, ph1);
       if (me == c.root) return;
       {  // phase 2: every owner's tiles, owners interleaved (all links at once)
-        const OwnerRowMap<W> m{&v, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
+        const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -108,7 +110,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       if (c.coll == IpcColl::GATHER && me != c.root) return;
       {
-        const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(me + b), b, G, nt};
+        const PeerTileMap<W> m{&v, &c, poff, c.bytes, (uint32_t)(me + b), b, G, nt};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -117,7 +119,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       if (me == c.root)
         for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
-      const OneSrcMap m{v.buf[c.root] + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
+      const OneSrcMap m{v.buf[c.root] + poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
@@ -125,7 +127,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       {
-        const PeerTileMap<W> m{&v, &c, me * cpad, c.bytes, (uint32_t)(me + b), b, G, nt};
+        const PeerTileMap<W> m{&v, &c, poff + me * cpad, c.bytes, (uint32_t)(me + b), b, G, nt};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -228,7 +230,8 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
   return hipSuccess;
 }
 
-size_t ipc_signal_bytes() { return (size_t)kMaxBlocks * kMaxRanks * sizeof(uint32_t); }
+// block-pairwise flags, then the sequence counter (kSeqWord) and arrivals (kArriveWord)
+size_t ipc_signal_bytes() { return (size_t)(kArriveWord + 16) * sizeof(uint32_t); }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;

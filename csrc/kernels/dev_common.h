@@ -328,6 +328,36 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
 }
 
 // ----------------------------------------------------------------------------
+// Sequence number of this IPC call (see kern::IpcView). Host-issued launches
+// pass it in the view and block 0 records it in the device counter. Graph-
+// captured launches read counter + 1 in every block; each block then arrives on
+// a counter with a release-ordered RMW (after its read), and the last arriver
+// resets the arrivals and publishes the new number for the next launch, so no
+// block can see it early. Uncached signal memory: no stale L2 line on any XCD.
+__device__ __forceinline__ uint32_t call_seq(const kern::IpcView& v) {
+  __shared__ uint32_t s_seq;
+  if (threadIdx.x == 0) {
+    uint32_t s;
+    uint32_t* const word = v.seq_dev + kern::kSeqWord;
+    if (v.dev_seq) {
+      uint32_t* const arrive = v.seq_dev + kern::kArriveWord;
+      s = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      const uint32_t n = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (n == gridDim.x - 1) {
+        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(word, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      s = v.seq;
+      if (blockIdx.x == 0) __hip_atomic_store(word, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_seq = s;
+  }
+  __syncthreads();
+  return s_seq;
+}
+
+// ----------------------------------------------------------------------------
 // K4: cross-GPU block-pairwise barrier.
 //
 // flags layout (per rank, uncached device memory): flags[block * kMaxRanks + src].

@@ -70,14 +70,26 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 
 // ---------------------------------------------------------------- IPC collectives
 // Per-rank view of the group's registered (hipIpc) memory for ONE call.
+//
+// The call's sequence number picks the staging parity (seq & 1) and the flag
+// epochs (2 seq, 2 seq + 1). Host-issued launches carry it in `seq`. A hipGraph
+// replays kernel arguments verbatim, so launches captured into a graph set
+// `dev_seq` and every block derives the number from the rank's own device
+// counter instead (seq_dev[kSeqWord] + 1; the last block to arrive publishes
+// it). Host-issued launches keep that counter current, so a group can switch
+// to graph mode at any call.
+constexpr int kSeqWord = kMaxBlocks * kMaxRanks;  // u32 index of the counter in the signal area
+constexpr int kArriveWord = kSeqWord + 16;        // arrivals of the current graph-mode launch
 struct IpcView {
-  char* buf[kMaxRanks];        // staging buffer of this call's parity, per rank (own included)
+  char* buf[kMaxRanks];        // staging buffer (parity 0; parity 1 starts at + cap), per rank (own included)
   uint32_t* flags[kMaxRanks];  // signal area (uncached device memory) per rank
   uint32_t* err;               // host-mapped error word (0 = ok), written on spin timeout
+  uint32_t* seq_dev;           // own signal area (sequence counter at kSeqWord, arrivals at kArriveWord)
+  size_t cap;                  // bytes per staging parity
   int rank;
   int world;
-  uint32_t seq;                // call sequence number (>= 1), identical on every rank
-  uint32_t pad_;
+  uint32_t seq;                // host-issued call sequence number, identical on every rank
+  uint32_t dev_seq;            // 1: graph-captured launch, take the number from seq_dev
   uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
 };
 

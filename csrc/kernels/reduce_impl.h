@@ -138,6 +138,7 @@ constexpr int kCopyDepth = 4;
 template <int W>
 struct OwnerRowMap {
   const IpcView* v;
+  size_t poff;  // staging parity offset of this call
   char* d;
   size_t dlim;
   uint32_t rot;
@@ -151,7 +152,7 @@ struct OwnerRowMap {
   __device__ const char* src(int, size_t i) const {
     int q;
     const size_t t = tile(i, q);
-    return v->buf[q] + t * kTile;
+    return v->buf[q] + poff + t * kTile;
   }
   __device__ char* dst(size_t i) const {
     int q;
@@ -170,7 +171,7 @@ template <int W>
 struct PeerTileMap {
   const IpcView* v;
   const IpcCall* c;
-  size_t sbase;
+  size_t sbase;  // parity offset + chunk offset inside each staging buffer
   size_t dlim;
   uint32_t rot;
   size_t first, stride, ntiles;
@@ -203,8 +204,10 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, D>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t ph0 = v.seq * 2u, ph1 = v.seq * 2u + 1u;
-  char* mine = v.buf[me];
+  const uint32_t seq = call_seq(v);
+  const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
+  const size_t poff = (seq & 1u) ? v.cap : 0;
+  char* mine = v.buf[me] + poff;
   const size_t nt = pad_tiles(c.bytes) / kTile;
 
   switch (c.coll) {
@@ -213,7 +216,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       if (c.coll == IpcColl::REDUCE_1SHOT && me != c.root) return;
-      const AllSrcMap<W> m{&v, 0, (char*)c.out[0], c.bytes, b, G, nt};
+      const AllSrcMap<W> m{&v, poff, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       return;
     }
@@ -224,14 +227,14 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       // phase 1: reduce my owned tiles from every rank, in place into my staging
       {
-        const AllSrcMap<W> m{&v, 0, mine, nt * kTile, me + W * b, W * G, nt};
+        const AllSrcMap<W> m{&v, poff, mine, nt * kTile, me + W * b, W * G, nt};
         pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       }
       block_barrier(v, ph1);
       if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
       // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
       {
-        const OwnerRowMap<W> m{&v, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
+        const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -240,7 +243,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       const size_t cpad = pad_tiles(c.bytes);
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
-      const AllSrcMap<W> m{&v, me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
+      const AllSrcMap<W> m{&v, poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       return;
     }

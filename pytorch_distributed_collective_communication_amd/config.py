@@ -8,6 +8,8 @@ group is constructed; :func:`current` shows what a new group would use and
 |---|---|---|
 | PDCC_ALGO | auto | force ``rccl`` / ``ipc`` / ``host`` for GPU tensors (preferred if feasible) |
 | PDCC_IPC | 1 | enable the hipIpc peer-memory path |
+| PDCC_IPC_SELFTEST | 1 | run the IPC protocol once on known data when a group first uses a GPU; any failure on any rank disables IPC for that group |
+| PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers |
 | PDCC_IPC_1SHOT_MAX | 512K | all-reduce/reduce/broadcast up to this size: 1-shot protocol |
 | PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
@@ -52,6 +54,8 @@ def parse_bytes(v: str | int) -> int:
 class Config:
     algo: str = "auto"
     ipc: bool = True
+    ipc_selftest: bool = True
+    ipc_selftest_ms: int = 20000
     ipc_1shot_max: int = 512 << 10
     ipc_2shot_max: int = 8 << 20
     ipc_copy_max: int = 1 << 20
@@ -74,7 +78,8 @@ class Config:
 
 
 _ENV = {
-    "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
+    "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_selftest": "PDCC_IPC_SELFTEST",
+    "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",

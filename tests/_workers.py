@@ -441,6 +441,68 @@ def autotune_probe(rank, size, device="cuda"):
     return {"ok": ok, "table": be.autotune_table()}
 
 
+def graph_capture(rank, size, device="cuda", replays=5):
+    """Collectives captured into a hipGraph (parallel.graphs.capture) and replayed
+    with new inputs each time, with an eager collective between two replays: the
+    IPC kernels' device-side sequence numbers must keep every rank's flag epochs
+    and staging parities in step across replays and eager calls."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel.graphs import capture
+
+    d = _dev(device)
+    small = torch.zeros(1000, device=d)      # IPC 1-shot
+    mid = torch.zeros(300_000, device=d)     # 1.2 MB: IPC 2-shot (RCCL at world 1)
+    bc = torch.zeros(5000, device=d)
+    ag_in = torch.zeros(780, device=d)
+    ag_out = torch.zeros(780 * size, device=d)
+
+    def fill(i):
+        small.fill_(float(rank + i))
+        mid.fill_(float(2 * rank + i))
+        bc.fill_(float(100 + i) if rank == 0 else -1.0)
+        ag_in.fill_(float(10 * rank + i))
+
+    def step():
+        dist.all_reduce(small)
+        dist.all_reduce(mid)
+        dist.broadcast(bc, src=0)
+        dist.all_gather_into_tensor(ag_out, ag_in)
+
+    fill(0)
+    g = capture(step, warmup=2)
+    ok = []
+    tri = size * (size - 1) / 2
+    for i in range(1, replays + 1):
+        fill(i)
+        g.replay()
+        if i == 3:  # an eager collective between two replays
+            e = torch.full((4096,), float(rank), device=d)
+            dist.all_reduce(e)
+            ok.append(bool(torch.all(e == tri).item()))
+        torch.cuda.synchronize()
+        ok.append(bool(torch.all(small == tri + size * i).item()))
+        ok.append(bool(torch.all(mid == 2 * tri + size * i).item()))
+        ok.append(bool(torch.all(bc == 100 + i).item()))
+        exp = torch.arange(size, device=d, dtype=torch.float32).repeat_interleave(780) * 10 + i
+        ok.append(bool(torch.equal(ag_out, exp)))
+    return ok
+
+
+def ipc_selftest_probe(rank, size, device="cuda"):
+    """One GPU all_reduce; returns (correct, whether the group kept the IPC path)."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    x = torch.full((1000,), float(rank + 1), device=_dev(device))
+    dist.all_reduce(x)
+    ok = bool(torch.all(x == size * (size + 1) / 2).item())
+    return ok, "ipc_ok=1" in be.describe()
+
+
 def gpu_fault_victim(rank, size, q, group_timeout_s=4):
     """Two ranks on the IPC path; rank 1 dies after setup. Rank 0's next GPU
     all_reduce spins in the cross-GPU barrier until the group timeout (bounded

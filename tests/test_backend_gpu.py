@@ -124,6 +124,25 @@ def test_autotuner_shared_gpu():
         assert e["algo"] in ("ipc", "host")
 
 
+@pytest.mark.parametrize("world,env", [
+    (1, {"PDCC_WORLD1_LOCAL": "0"}),                           # RCCL graph nodes
+    (2, {"PDCC_ALGO": "ipc"}),                                 # IPC kernels, device-side sequence numbers
+    (2, {}),                                                   # autotuned choices (host engine -> IPC)
+    (3, {"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": "0"}),      # 2-shot everywhere, partial rows
+])
+def test_graph_capture_and_replay(world, env):
+    for ok in _gpu_launch(W.graph_capture, world, env=env):
+        assert all(ok), ok
+
+
+@pytest.mark.parametrize("fail_rank", ["", "1"])
+def test_ipc_selftest_gates_the_peer_memory_path(fail_rank):
+    env = {"PDCC_IPC_SELFTEST_FAIL": fail_rank} if fail_rank else {}
+    for ok, ipc_on in _gpu_launch(W.ipc_selftest_probe, 2, env=env):
+        assert ok
+        assert ipc_on == (not fail_rank)
+
+
 def test_gpu_peer_death_is_detected():
     import os
 
