@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_BUSBW = {2: 6.14, 4: 5.49, 8: 3.16}  # BASELINE.md §2.1 (reference stack, Gloo/CPU)
+BASELINE_P50_MS = {1: 0.027, 2: 174.8, 4: 293.4, 8: 595.1}  # same table, p50 latency
 SMALL = os.environ.get("PDCC_BENCH_SMALL", "0") == "1"  # functional rehearsal sizes for the extras
 NBYTES = 1 << 30
 EXTRAS_PARTIAL: dict = {}  # run_extras fills this in place (reported even if a deadline fires)
@@ -143,6 +144,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "p50_ms": round(p50 * 1e3, 4),
+            "baseline_p50_ms": BASELINE_P50_MS.get(world),
             "busbw_p50_GBps": round(busbw(args.bytes, world, p50), 3),
             "algbw_GBps": round(args.bytes / (ms_per_step / 1e3) / 1e9, 3) if world > 1 else None,
             "higher_is_better": True,
@@ -296,7 +298,39 @@ def run_extras(world, rank, dev, native, x):
             out["baseline_configs"] = baseline_configs(world, rank, dev, x)
         except Exception as e:
             out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
+        out.update(graph_replay(world, rank, dev))
     return out
+
+
+def graph_replay(world, rank, dev, n_ops=16, numel=1024):
+    """hipGraph replay vs eager issue of a launch-bound step: n_ops small
+    all_reduces captured with parallel.graphs.capture, checked afterwards."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel.graphs import capture
+
+    res = {}
+    tag = f"graph_{n_ops}x{numel * 4}B_allreduce"
+    try:
+        progress("graph replay vs eager")
+        bufs = [torch.zeros(numel, device=dev) for _ in range(n_ops)]
+
+        def step():
+            for b in bufs:
+                dist.all_reduce(b)
+
+        res[f"{tag}_eager_us"] = round(_time_op(step, 20) * 1e6, 1)
+        g = capture(step, warmup=2)
+        res[f"{tag}_replay_us"] = round(_time_op(g.replay, 20) * 1e6, 1)
+        for b in bufs:
+            b.fill_(float(rank + 1))
+        g.replay()
+        torch.cuda.synchronize()
+        res[f"{tag}_correct"] = all(bool(torch.all(b == world * (world + 1) / 2).item()) for b in bufs)
+    except Exception as e:
+        res["graph_error"] = f"{type(e).__name__}: {e}"[:300]
+    return res
 
 
 def progress(msg):

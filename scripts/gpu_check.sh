@@ -16,9 +16,11 @@ step() {  # step <name> <seconds> <cmd...>
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python __graft_entry__.py ;;
-    kern) step kern 600 python -m pytest tests/test_kernels_gpu.py -x -q ;;
-    backend) step backend 900 python -m pytest tests/test_backend_gpu.py -x -q ;;
-    gputests) step gputests 1200 python -m pytest tests -m gpu -q ;;
+    kern) step kern 600 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread ;;
+    backend) step backend 900 python -u -m pytest tests/test_backend_gpu.py -x -v --timeout 300 --timeout-method thread ;;
+    gputests) step gputests 1200 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+    graphbench) step graphbench 300 python scripts/graph_bench.py ;;
+    graphbench1) GRAPH_BENCH_MODE=rccl1 step graphbench1 300 python scripts/graph_bench.py ;;
     bench1) step bench1 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench2dbg) PDCC_BENCH_SMALL=1 PDCC_LOG_LEVEL=2 PDCC_BENCH_DEBUG_S=150 step bench2dbg 240 \
         python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
