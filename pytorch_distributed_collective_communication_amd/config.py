@@ -9,7 +9,8 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_ALGO | auto | force ``rccl`` / ``ipc`` / ``host`` for GPU tensors (preferred if feasible) |
 | PDCC_IPC | 1 | enable the hipIpc peer-memory path |
 | PDCC_IPC_SELFTEST | 1 | run the IPC protocol once on known data when a group first uses a GPU; any failure on any rank disables IPC for that group |
-| PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers |
+| PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers (capped by the group timeout) |
+| PDCC_IPC_SELFTEST_FAIL | "" | test hook: this rank reports a failed self-test |
 | PDCC_IPC_1SHOT_MAX | 512K | all-reduce/reduce/broadcast up to this size: 1-shot protocol |
 | PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
