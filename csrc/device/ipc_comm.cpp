@@ -42,6 +42,37 @@ std::pair<void*, void*> open_handle(const std::vector<uint8_t>& b) {
   return {p, static_cast<char*>(p) + off};
 }
 
+// Allocate `bytes` of device memory and export it. With two ranks on one device
+// the runtime can hand back a range it just unmapped for a closed peer import,
+// and then refuses to export it (hipIpcGetMemHandle: invalid argument). Such a
+// block is held (so the next try gets a different range) and freed once an
+// exportable one is found. `uncached` selects fine-grained memory (signals).
+void* alloc_exportable(size_t bytes, bool uncached, std::vector<uint8_t>& blob) {
+  std::vector<void*> refused;
+  auto release = [&] {
+    for (void* q : refused) hipFree(q);
+  };
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    void* p = nullptr;
+    hipError_t e = uncached ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) : hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      release();
+      PDCC_HIP(e);
+    }
+    try {
+      blob = handle_bytes(p);
+      release();
+      return p;
+    } catch (const std::exception&) {
+      (void)hipGetLastError();
+      refused.push_back(p);
+    }
+  }
+  release();
+  throw std::runtime_error("pdcc: hipIpcGetMemHandle refused 6 fresh allocations of " + std::to_string(bytes) +
+                           " bytes");
+}
+
 // own allocations in whole 2 MiB granules, so the runtime never packs two of
 // them (or anybody else's) into one IPC-exported allocation
 constexpr size_t kGranule = 2u << 20;
@@ -84,13 +115,12 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   std::string err;
   try {
     const size_t sig = granule(kern::ipc_signal_bytes());
-    PDCC_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&my_flags_), sig, hipDeviceMallocUncached));
+    my_flags_ = static_cast<uint32_t*>(alloc_exportable(sig, true, mine));
     PDCC_HIP(hipMemset(my_flags_, 0, sig));
     PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
     *err_host_ = 0;
     PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
     PDCC_HIP(hipDeviceSynchronize());
-    mine = handle_bytes(my_flags_);
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();  // published empty: the peers fail this step with us
@@ -146,15 +176,19 @@ void IpcComm::unmap_staging() {
 }
 
 void IpcComm::map_staging(size_t cap) {
+  // the new buffer is allocated and exported while the old one and the peers'
+  // old mappings still hold their ranges, so it cannot land on a just-closed import
   std::vector<uint8_t> mine;
   std::string err;
+  char* fresh = nullptr;
   try {
-    PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&my_staging_), granule(2 * cap)));
-    mine = handle_bytes(my_staging_);
+    fresh = static_cast<char*>(alloc_exportable(granule(2 * cap), false, mine));
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();
   }
+  unmap_staging();
+  my_staging_ = fresh;
   const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_, mine);
   try {
     if (!err.empty()) throw std::runtime_error(err);
@@ -189,7 +223,6 @@ void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
   PDCC_HIP(hipStreamSynchronize(stream));
   ++staging_gen_;
   store_barrier(store_, key_ + "/ipc_grow/" + std::to_string(staging_gen_), rank_, world_);
-  unmap_staging();
   map_staging(cap);
 }
 

@@ -383,6 +383,27 @@ def two_groups(rank, size, device="cuda"):
     return ok
 
 
+def staging_growth(rank, size, device="cuda", max_bytes=64 << 20):
+    """all_reduce with sizes doubling from 4 KiB to `max_bytes` on the world
+    group, then on a second group: every doubling regrows the IPC staging
+    (regression: with ranks sharing a device, a fresh allocation could land on a
+    just-closed peer import and hipIpcGetMemHandle refused to export it)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    g = dist.new_group(list(range(size)))
+    ok = []
+    for grp in (None, g):
+        n = 1024
+        while n * 4 <= max_bytes:
+            x = torch.full((n,), float(rank + 1), device=d)
+            dist.all_reduce(x, group=grp)
+            ok.append(bool(torch.all(x == size * (size + 1) / 2).item()))
+            n *= 2
+    return ok
+
+
 def async_ordering(rank, size, device="cuda", rounds=20):
     """async_op=True collectives run on the backend's comm stream: the hand-off
     from the caller's stream (producer kernels still running) and back (Work.wait

@@ -101,6 +101,11 @@ def test_two_ipc_groups_in_one_process():
         assert all(ok), ok
 
 
+def test_ipc_staging_regrowth_two_groups():
+    for ok in _gpu_launch(W.staging_growth, 2, env={"PDCC_ALGO": "ipc"}):
+        assert len(ok) == 30 and all(ok), ok
+
+
 @pytest.mark.parametrize("world,stream", [(1, "auto"), (1, "comm"), (2, "auto"), (2, "comm")])
 def test_async_ops_stream_ordering(world, stream):
     env = {"PDCC_STREAM": stream, "PDCC_WORLD1_LOCAL": "0"}
