@@ -64,6 +64,10 @@ Config Config::from_env() {
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
   c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
+  c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
+  c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
+  if (c.rccl_min_ctas > 0 && c.rccl_max_ctas > 0 && c.rccl_min_ctas > c.rccl_max_ctas)
+    throw std::runtime_error("PDCC_RCCL_MIN_CTAS must not exceed PDCC_RCCL_MAX_CTAS");
   c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
   if (const char* sm = env("PDCC_STREAM")) {
     std::string v(sm);
@@ -90,7 +94,7 @@ std::string Config::describe() const {
   o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_selftest=" << ipc_selftest
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
-    << " ipc_max_staging=" << ipc_max_staging << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
+    << " ipc_max_staging=" << ipc_max_staging << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
     << " watchdog_ms=" << watchdog_ms << " stream=" << (stream_mode == 0 ? "auto" : stream_mode == 1 ? "high" : stream_mode == 2 ? "comm" : "current");
   return o.str();

@@ -37,6 +37,11 @@ struct Config {
   // (Measured on MI355X: a cross-stream event hand-off costs ~20 us per op on a normal
   // stream and ~150 us on a high-priority one; the caller's stream ~5 us end to end.)
   int stream_mode = 0;
+  // RCCL channel tuning: each CTA drives one channel (ring/tree lane); on 8 GPUs one
+  // channel per xGMI link needs >= 7. -1 leaves RCCL's own topology tuner in charge
+  // (ncclCommInitRank); any value set goes through ncclCommInitRankConfig.
+  int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
+  int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
   bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
   // host transport
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES

@@ -203,7 +203,8 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
 
 RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
   if (!ds.rccl) {
-    auto c = std::make_unique<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device);
+    auto c = std::make_unique<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device, cfg_.rccl_min_ctas,
+                                        cfg_.rccl_max_ctas);
     std::lock_guard<std::mutex> lk(init_mu_);
     ds.rccl = std::move(c);
   }

@@ -8,7 +8,7 @@
 namespace pdcc {
 
 RcclComm::RcclComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world,
-                   int device)
+                   int device, int min_ctas, int max_ctas)
     : device_(device) {
   ncclUniqueId id;
   const std::string k = key + "/rccl_uid";
@@ -23,7 +23,14 @@ RcclComm::RcclComm(const c10::intrusive_ptr<c10d::Store>& store, const std::stri
   int prev = 0;
   PDCC_HIP(hipGetDevice(&prev));
   PDCC_HIP(hipSetDevice(device));
-  PDCC_NCCL(ncclCommInitRank(&comm_, world, id, rank));
+  if (min_ctas > 0 || max_ctas > 0) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (min_ctas > 0) cfg.minCTAs = min_ctas;
+    if (max_ctas > 0) cfg.maxCTAs = max_ctas;
+    PDCC_NCCL(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg));
+  } else {
+    PDCC_NCCL(ncclCommInitRank(&comm_, world, id, rank));
+  }
   PDCC_HIP(hipSetDevice(prev));
 }
 

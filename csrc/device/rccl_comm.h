@@ -23,7 +23,8 @@ namespace pdcc {
 class RcclComm {
  public:
   // Collective over the group: rank 0 creates the unique id and publishes it.
-  RcclComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world, int device);
+  RcclComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world, int device,
+           int min_ctas = -1, int max_ctas = -1);
   ~RcclComm();
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;

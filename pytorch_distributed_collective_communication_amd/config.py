@@ -17,6 +17,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_MAX_STAGING | 512M | staging bytes per parity; larger calls are chunked |
 | PDCC_AUTOTUNE | 1 | GPU all_reduce: time RCCL vs IPC on the first call per power-of-two size bucket (IPC result checked against RCCL's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4G | size range the autotuner covers (outside: the static thresholds) |
+| PDCC_RCCL_MIN_CTAS / _MAX_CTAS | -1 / -1 | RCCL channel (CTA) bounds via ``ncclCommInitRankConfig``; -1 leaves RCCL's topology tuner in charge |
 | PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
@@ -64,6 +65,8 @@ class Config:
     autotune: bool = True
     autotune_min: int = 64 << 10
     autotune_max: int = 4 << 30
+    rccl_min_ctas: int = -1
+    rccl_max_ctas: int = -1
     world1_local: bool = True
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
@@ -84,6 +87,7 @@ _ENV = {
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
+    "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
     "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
     "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",

@@ -33,6 +33,13 @@ def test_world1_rccl_bulk_paths():
     assert all(res[0].values()), res[0]
 
 
+def test_world1_rccl_with_cta_config():
+    # ncclCommInitRankConfig path (channel bounds) on a 1-rank communicator
+    env = {"PDCC_WORLD1_LOCAL": "0", "PDCC_RCCL_MIN_CTAS": "8", "PDCC_RCCL_MAX_CTAS": "32"}
+    res = _gpu_launch(W.large, 1, env=env)
+    assert all(res[0].values()), res[0]
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_shared_gpu_ipc_golden(world):
     res = _gpu_launch(W.golden, world, env={"PDCC_ALGO": "ipc"})

@@ -15,6 +15,15 @@ def test_parse_bytes():
     assert config.parse_bytes("4096") == 4096
 
 
+def test_config_rccl_cta_knobs():
+    from pytorch_distributed_collective_communication_amd import config
+
+    c = config.current({"PDCC_RCCL_MIN_CTAS": "8", "PDCC_RCCL_MAX_CTAS": "32"})
+    assert (c.rccl_min_ctas, c.rccl_max_ctas) == (8, 32)
+    assert config.current({}).rccl_min_ctas == -1
+    assert config.env_for(rccl_max_ctas=14) == {"PDCC_RCCL_MAX_CTAS": "14"}
+
+
 def test_config_current_and_env_for():
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_2SHOT_MAX": "16M", "PDCC_DEBUG": "1", "PDCC_IPC": "0"}
     c = config.current(env)
