@@ -1,9 +1,15 @@
 #!/usr/bin/env python3
 """Headline benchmark: all_reduce busbw + p50 latency, 1 GiB fp32 (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]            # N=1 (default)
+    python bench.py [--gpus N] [--steps K] [--warmup W]            # starts N ranks itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
-        --master-addr 127.0.0.1 --master-port P bench.py --gpus N  # N>1
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N  # or under torchrun
+
+Without a torchrun environment (no WORLD_SIZE) and N > 1 the script is its own
+launcher (``launch_ranks``): it starts N child ranks on a free 127.0.0.1 port,
+makes no GPU call itself, and propagates the first failing rank's exit code.
+``PDCC_BENCH_DEVICE=cpu`` runs the same harness on CPU tensors through the
+backend's host transport (functional rehearsal, used by the CPU test suite).
 
 One rank per GPU, backend ``mi355x`` (this library). A "step" is one in-place
 ``dist.all_reduce(SUM)`` of a 1 GiB fp32 tensor (268,435,456 synthetic random
@@ -42,14 +48,81 @@ def busbw(nbytes: int, n: int, sec: float) -> float:
     return 0.0 if n <= 1 or sec <= 0 else nbytes * 2 * (n - 1) / n / sec / 1e9
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=NBYTES)
     ap.add_argument("--extras", type=int, default=int(os.environ.get("PDCC_BENCH_EXTRAS", "1")))
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """``python bench.py --gpus N`` without a torchrun environment: start N
+    ranks of this script as child processes (one per GPU, LOCAL_RANK = rank),
+    the way the reference's ``__main__`` starts its workers (main.py:98-108) but
+    with exit codes checked. This parent makes no GPU call and never imports
+    torch; it waits for the ranks, and if one fails or the deadline passes it
+    stops the others and exits non-zero. Only rank 0 prints the JSON line (the
+    children share this process's stdout)."""
+    import signal
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    deadline = time.time() + float(os.environ.get("PDCC_BENCH_TIMEOUT_S", "1500"))
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, c = bad[0]
+            print(f"[bench] rank {r} exited with code {c}; stopping the other ranks", file=sys.stderr, flush=True)
+            rc = c if c > 0 else 128 - c
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() > deadline:
+            print("[bench] deadline passed; stopping the ranks", file=sys.stderr, flush=True)
+            rc = 124
+            break
+        time.sleep(0.1)
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    t_end = time.time() + 15
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, argv))
+    run_rank(args)
+
+
+def run_rank(args):
     if os.environ.get("PDCC_BENCH_DEBUG_S"):
         import faulthandler
 
@@ -66,17 +139,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    ngpu = torch.cuda.device_count()
-    local = local % ngpu  # (ranks > GPUs only in functional rehearsals on a 1-GPU box)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    on_gpu = os.environ.get("PDCC_BENCH_DEVICE", "cuda") != "cpu"
+    if on_gpu:
+        ngpu = torch.cuda.device_count()
+        local = local % ngpu  # (ranks > GPUs only in functional rehearsals on a 1-GPU box)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:  # functional rehearsal of the whole harness on the host transport (tests)
+        dev = torch.device("cpu")
+        torch.set_num_threads(1)
+    csync = torch.cuda.synchronize if on_gpu else (lambda: None)
     if world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if "MASTER_PORT" not in os.environ:
-            from pytorch_distributed_collective_communication_amd.parallel.spawn import free_port
-
-            os.environ["MASTER_PORT"] = str(free_port())
+            os.environ["MASTER_PORT"] = str(_free_port())
     dist.init_process_group("mi355x", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=10))
     native = be.native_backend()
 
@@ -86,7 +163,7 @@ def main():
 
     def sync():
         dist.barrier()
-        torch.cuda.synchronize()
+        csync()
 
     def max_over_ranks(v: float) -> float:
         t = torch.tensor([v], dtype=torch.float64)
@@ -103,9 +180,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         dist.all_reduce(x)
-    torch.cuda.synchronize()
+    csync()
     dist.barrier()
-    torch.cuda.synchronize()
+    csync()
     total = max_over_ranks(time.perf_counter() - t0)
     ar = {k: v[0] for k, v in native.stats().items() if k.startswith("allreduce/")}
     algo = max(ar, key=ar.get).split("/", 1)[1] if ar else "?"
@@ -117,7 +194,7 @@ def main():
         sync()
         s0 = time.perf_counter()
         dist.all_reduce(x)
-        torch.cuda.synchronize()
+        csync()
         lat.append(max_over_ranks(time.perf_counter() - s0))
     p50 = statistics.median(lat)
 
@@ -151,7 +228,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_BUSBW[world], 2) if world in BASELINE_BUSBW else None,
             "dtype": "fp32",
-            "data": "synthetic (torch.rand, 1 GiB per rank)",
+            "data": f"synthetic (torch.rand, {args.bytes} bytes fp32 per rank, random-init; no dataset)",
             "config": {
                 "model": "all_reduce SUM 1 GiB fp32 (reference main.py do_all_reduce, scaled to BASELINE.json)",
                 "global_batch": world,
@@ -159,6 +236,7 @@ def main():
                 "parallelism": f"dp{world}",
                 "backend": "mi355x",
                 "algo": algo,
+                "device": dev.type,
             },
             "correct": correct,
             "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
@@ -179,7 +257,7 @@ def main():
         os._exit(0)
 
     extras = {}
-    if args.extras:
+    if args.extras and on_gpu:
         timer = threading.Timer(float(os.environ.get("PDCC_BENCH_EXTRAS_S", "300")), deadline, args=("extras",))
         timer.daemon = True
         timer.start()

@@ -1,0 +1,45 @@
+"""bench.py as the driver starts it: ``python bench.py --gpus N`` with no torchrun
+environment must launch its own N ranks (reference main.py:98-108 pattern), print
+exactly one JSON line from rank 0, and propagate a failing rank's exit code
+instead of hanging. Rehearsed on CPU tensors (PDCC_BENCH_DEVICE=cpu, host
+transport) so it runs without a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=240):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env.update({"PDCC_BENCH_DEVICE": "cpu", "PDCC_BENCH_TIMEOUT_S": "180"})
+    env.update(extra_env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_bench_self_launch_prints_one_line(n):
+    r = _run(["--gpus", str(n), "--bytes", "4096", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == n and rec["steps"] == 2 and rec["warmup"] == 1
+    assert rec["correct"] is True
+    assert rec["config"]["parallelism"] == f"dp{n}"
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    if n > 1:
+        assert rec["value"] > 0 and rec["vs_baseline"] is not None
+
+
+def test_bench_failing_rank_propagates():
+    # rank 1 dies at its 3rd collective: the launcher must stop rank 0 and exit non-zero
+    r = _run(["--gpus", "2", "--bytes", "4096", "--steps", "2", "--warmup", "1"], {"PDCC_FAULT": "1:3:exit"})
+    assert r.returncode != 0
+    assert "rank 1 exited" in r.stderr
