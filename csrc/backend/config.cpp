@@ -1,5 +1,6 @@
 #include "config.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <sstream>
 #include <stdexcept>
@@ -64,6 +65,45 @@ Config Config::from_env() {
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
   c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
+  c.autotune_sample = std::max<size_t>(env_size("PDCC_AUTOTUNE_SAMPLE", c.autotune_sample), 64u << 10);
+  if (const char* ac = env("PDCC_AUTOTUNE_COLLS")) {
+    static const char* kNames[] = {"allreduce", "reduce", "broadcast", "allgather", "gather",
+                                   "scatter", "reduce_scatter", "alltoall"};
+    c.autotune_colls = 0;
+    std::string s(ac);
+    size_t pos = 0;
+    while (pos <= s.size()) {
+      const size_t e = std::min(s.find(',', pos), s.size());
+      const std::string tok = s.substr(pos, e - pos);
+      bool known = tok.empty() || tok == "none";
+      if (tok == "all") {
+        c.autotune_colls = 0xffffffffu;
+        known = true;
+      }
+      for (int i = 0; i < 8; ++i)
+        if (tok == kNames[i]) {
+          c.autotune_colls |= 1u << i;
+          known = true;
+        }
+      if (!known) throw std::runtime_error("PDCC_AUTOTUNE_COLLS: unknown collective '" + tok + "'");
+      pos = e + 1;
+    }
+  }
+  c.ipc_spin_ms = (int64_t)env_size("PDCC_IPC_SPIN_MS", (size_t)c.ipc_spin_ms);
+  if (const char* gc = env("PDCC_RCCL_GROUP_COMM")) {
+    std::string v(gc);
+    if (v == "split") c.group_comm = 0;
+    else if (v == "share") c.group_comm = 1;
+    else if (v == "init") c.group_comm = 2;
+    else throw std::runtime_error("PDCC_RCCL_GROUP_COMM must be split|share|init, got " + v);
+  }
+  c.rccl_split_share = env_bool("PDCC_RCCL_SPLIT_SHARE", c.rccl_split_share);
+  if (const char* lg = env("PDCC_LIST_GATHER")) {
+    std::string v(lg);
+    if (v == "p2p") c.list_gather_p2p = true;
+    else if (v == "staged") c.list_gather_p2p = false;
+    else throw std::runtime_error("PDCC_LIST_GATHER must be p2p|staged, got " + v);
+  }
   c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
   c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
   if (c.rccl_min_ctas > 0 && c.rccl_max_ctas > 0 && c.rccl_min_ctas > c.rccl_max_ctas)
@@ -94,7 +134,11 @@ std::string Config::describe() const {
   o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_selftest=" << ipc_selftest
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
-    << " ipc_max_staging=" << ipc_max_staging << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
+    << " ipc_max_staging=" << ipc_max_staging << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
+    << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas
+    << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
+    << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
+    << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
     << " watchdog_ms=" << watchdog_ms << " stream=" << (stream_mode == 0 ? "auto" : stream_mode == 1 ? "high" : stream_mode == 2 ? "comm" : "current");
   return o.str();

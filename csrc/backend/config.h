@@ -25,12 +25,21 @@ struct Config {
   // topology the protocol does not work on falls back to RCCL instead of hanging or corrupting data.
   bool ipc_selftest = true;                // PDCC_IPC_SELFTEST
   int ipc_selftest_ms = 20000;             // PDCC_IPC_SELFTEST_MS spin timeout during the self-test
+  // Upper bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if
+  // shorter); the watchdog's abort stops a spin at once.
+  int64_t ipc_spin_ms = 600000;            // PDCC_IPC_SPIN_MS
   // Online autotuner (GPU all_reduce, groups where both RCCL and IPC are feasible): the first call
   // in each power-of-two size bucket >= autotune_min runs both engines on scratch copies, checks
   // that the IPC result matches RCCL's, times both and adopts the faster one on every rank.
+  // Every GPU collective with two feasible engines is tuned per (collective, dtype, op, size
+  // bucket); the key's first call pays it, later calls look the decision up.
   bool autotune = true;                    // PDCC_AUTOTUNE=0 keeps the static thresholds above
   size_t autotune_min = 64u << 10;         // PDCC_AUTOTUNE_MIN
-  size_t autotune_max = 4ull << 30;        // PDCC_AUTOTUNE_MAX (tuning clones the tensor twice)
+  size_t autotune_max = 1ull << 42;        // PDCC_AUTOTUNE_MAX
+  // Tuning runs on scratch buffers of at most this many bytes per engine (a prefix of the
+  // caller's data): above it both engines are bandwidth-bound, so the sample decides the bucket.
+  size_t autotune_sample = 1ull << 30;     // PDCC_AUTOTUNE_SAMPLE
+  uint32_t autotune_colls = 0xffffffffu;   // PDCC_AUTOTUNE_COLLS=allreduce,reduce,... (default all)
   // PDCC_STREAM: auto (default) = synchronous collectives (async_op=False) on the caller's stream,
   // async ones on a normal-priority comm stream; high = auto with a high-priority comm stream;
   // comm = always the comm stream; current = always the caller's stream.
@@ -42,6 +51,14 @@ struct Config {
   // (ncclCommInitRank); any value set goes through ncclCommInitRankConfig.
   int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
   int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
+  // Groups whose member set equals a live communicator's (new_group(range(size)) in every demo
+  // of the reference): split = ncclCommSplit from it (cheap), share = use the same communicator,
+  // init = always a fresh ncclCommInitRank.
+  int group_comm = 0;                      // PDCC_RCCL_GROUP_COMM=split|share|init (0|1|2)
+  bool rccl_split_share = true;            // PDCC_RCCL_SPLIT_SHARE: split children share parent resources
+  // all_gather into a list of separate tensors on RCCL: p2p = grouped ncclSend/Recv straight
+  // into the list (zero copy), staged = ncclAllGather into a staging buffer + K2 unpack
+  bool list_gather_p2p = true;             // PDCC_LIST_GATHER=p2p|staged
   bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
   // host transport
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES

@@ -1,22 +1,28 @@
 // GPU data paths of ProcessGroupMI355X.
 //
-// Every collective is enqueued on a per-device high-priority comm stream that
-// first waits (hipEvent) for the caller's current stream, exactly like the
-// reference's sync `dist.*` calls appear to the user (main.py:14-83) but without
-// blocking the host. Per call one of three engines runs:
+// Every collective runs on the caller's stream (synchronous ops) or on a
+// per-device comm stream that first waits for the caller's stream (async ops),
+// exactly like the reference's sync `dist.*` calls appear to the user
+// (main.py:14-83) but without blocking the host. Per call one of three engines:
 //   IPC  -- csrc/kernels: stage into own registered buffer, flag peers, pull or
 //           reduce straight from every peer's buffer over xGMI (1-/2-shot)
 //   RCCL -- ncclAllReduce/Reduce/Broadcast/AllGather/ReduceScatter/AllToAll and
-//           grouped ncclSend/Recv (gather/scatter/uneven all-to-all/p2p)
+//           grouped ncclSend/Recv (gather/scatter/list all-gather/uneven
+//           all-to-all straight into the caller's list tensors)
 //   HOST -- D2H, the shared-memory host transport, H2D (fallback only)
+// Which one: a static size threshold (config.h) until the online autotuner has
+// timed both feasible engines for the call's (collective, dtype, op, size
+// bucket) on this very node; from then on the measured winner.
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <sstream>
 
 #include "../device/comm_util.h"
 #include "process_group.h"
@@ -79,9 +85,26 @@ bool nccl_op(RedOpType op, at::ScalarType t, ncclRedOp_t& o) {
     case RedOpType::MIN: o = ncclMin; return true;
     case RedOpType::MAX: o = ncclMax; return true;
     case RedOpType::AVG: o = ncclAvg; return !b;
-    default: return false;
+    default: return false;  // BAND/BOR/BXOR: no RCCL op (IPC kernels or the host path)
   }
 }
+
+const char* op_name(int op) {
+  switch (op) {
+    case RedOpType::SUM: return "SUM";
+    case RedOpType::AVG: return "AVG";
+    case RedOpType::PRODUCT: return "PRODUCT";
+    case RedOpType::MIN: return "MIN";
+    case RedOpType::MAX: return "MAX";
+    case RedOpType::BAND: return "BAND";
+    case RedOpType::BOR: return "BOR";
+    case RedOpType::BXOR: return "BXOR";
+    default: return "?";
+  }
+}
+
+// tune-key "op" slot of the copy collectives: the output/input list layout
+constexpr int kLayoutFlat = 100, kLayoutList = 101;
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -131,6 +154,9 @@ bool capturing(hipStream_t s) {
 bool capturing_on(int device) {
   return capturing(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device).stream());
 }
+hipStream_t current_stream(int device) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device).stream();
+}
 
 // host path only competes for small messages, where its latency can beat a GPU protocol
 constexpr size_t kHostTuneMax = 4u << 20;
@@ -148,10 +174,74 @@ bool results_match(const at::Tensor& ref, const at::Tensor& got, RedOpType op, i
   return at::allclose(g, r, tol, tol * amax + 1e-30);
 }
 
+bool lists_equal(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (!at::equal(a[i], b[i])) return false;
+  return true;
+}
+
+// Elements of a tuning sample: at most `budget` bytes (per `units` tensors), a whole
+// number of 16-B vectors unless the full tensor fits.
+int64_t sample_numel(int64_t numel, size_t esize, size_t budget, int units = 1) {
+  const int64_t cap = (int64_t)(budget / std::max<size_t>(1, esize) / std::max(1, units));
+  if (numel <= cap) return numel;
+  const int64_t vec = std::max<int64_t>(1, 16 / (int64_t)esize);
+  return std::max<int64_t>(vec, cap / vec * vec);
+}
+
+// Read-only inputs for a tuning run: the first n elements of each tensor; a flat list
+// stays flat (copied into one allocation) so the timed path is the one the call takes.
+std::vector<at::Tensor> sample_inputs(const std::vector<at::Tensor>& v, int64_t n, bool flat) {
+  if (v.empty() || n >= v[0].numel()) return v;
+  std::vector<at::Tensor> out;
+  if (flat) {
+    at::Tensor buf = at::empty({(int64_t)v.size() * n}, v[0].options());
+    for (size_t i = 0; i < v.size(); ++i) {
+      out.push_back(buf.narrow(0, (int64_t)i * n, n));
+      out.back().copy_(v[i].reshape({-1}).narrow(0, 0, n));
+    }
+  } else {
+    for (const auto& t : v) out.push_back(t.reshape({-1}).narrow(0, 0, n));
+  }
+  return out;
+}
+// Scratch outputs for a tuning run, laid out like the caller's (flat or separate tensors).
+std::vector<at::Tensor> scratch_outputs(const at::TensorOptions& opt, size_t count, int64_t n, bool flat) {
+  std::vector<at::Tensor> out;
+  if (flat) {
+    at::Tensor buf = at::empty({(int64_t)count * n}, opt);
+    for (size_t i = 0; i < count; ++i) out.push_back(buf.narrow(0, (int64_t)i * n, n));
+  } else {
+    for (size_t i = 0; i < count; ++i) out.push_back(at::empty({n}, opt));
+  }
+  return out;
+}
+
+// Which groups may split from / share each other's RCCL communicator: same member set
+std::string members_key(const std::vector<int64_t>& global_ranks, int size) {
+  std::vector<int64_t> r = global_ranks;
+  if (r.empty())
+    for (int i = 0; i < size; ++i) r.push_back(i);
+  std::sort(r.begin(), r.end());
+  std::ostringstream o;
+  for (size_t i = 0; i < r.size(); ++i) o << (i ? "," : "") << r[i];
+  return o.str();
+}
+
+// IPC self-test verdicts of earlier groups with the same member set on the same devices:
+// the topology did not change, so later groups skip the test when every rank has one.
+std::mutex g_verdict_mu;
+std::map<std::string, bool> g_ipc_verdict;
+
 }  // namespace
 
+std::string ProcessGroupMI355X::make_members_key(const std::vector<int64_t>& global_ranks, int size) {
+  return members_key(global_ranks, size);
+}
+
 // =================================================================== device state
-DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
+DeviceState& ProcessGroupMI355X::dev_local(const at::Tensor& t) {
   const int d = t.device().index();
   std::lock_guard<std::mutex> lk(init_mu_);
   auto it = devs_.find(d);
@@ -159,14 +249,50 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   TORCH_CHECK(devs_.empty(), "pdcc: one GPU per rank per process group (got a tensor on cuda:", d,
               " after using cuda:", devs_.begin()->first, ")");
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)d);
+  auto ds = std::make_unique<DeviceState>(
+      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
+  ds->device = d;
+  DeviceState& ref = *ds;
+  devs_[d] = std::move(ds);
+  return ref;
+}
+
+DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
+  DeviceState& ds = dev_local(t);
+  std::lock_guard<std::mutex> lk(init_mu_);
+  if (!ds.topo) init_topology(ds);
+  return ds;
+}
+
+// Collective over the group (init_mu_ held): where is every rank, can RCCL run (one
+// rank per device) and can the IPC path run (same host, every peer reachable, and
+// the protocol self-test passes on this topology).
+void ProcessGroupMI355X::init_topology(DeviceState& ds) {
+  const int d = ds.device;
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)d);
   char bus[64] = {0};
   PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
   char host[256] = {0};
   gethostname(host, sizeof(host) - 1);
   const std::string rec = std::string(host) + "|" + bus;
-  const auto all = store_allgather(store_, "pdcc/dev", rank_, size_, std::vector<uint8_t>(rec.begin(), rec.end()));
+  const std::string vkey = members_key_ + "@" + rec;
+  char cached = '?';
+  {
+    std::lock_guard<std::mutex> lk(g_verdict_mu);
+    auto it = g_ipc_verdict.find(vkey);
+    if (it != g_ipc_verdict.end()) cached = it->second ? '1' : '0';
+  }
+  const std::string mine = rec + "#" + cached;
+  const auto all = store_allgather(store_, "pdcc/dev", rank_, size_, std::vector<uint8_t>(mine.begin(), mine.end()));
   std::vector<std::string> recs;
-  for (const auto& v : all) recs.emplace_back(v.begin(), v.end());
+  bool all_cached = true;
+  for (const auto& v : all) {
+    const std::string s(v.begin(), v.end());
+    const size_t h = s.rfind('#');
+    recs.push_back(s.substr(0, h));
+    const char c = h + 1 < s.size() ? s[h + 1] : '?';
+    all_cached = all_cached && c != '?' && c == cached;
+  }
   bool shared = false;
   for (int a = 0; a < size_; ++a)
     for (int b = a + 1; b < size_; ++b) shared = shared || recs[a] == recs[b];
@@ -187,34 +313,128 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
   for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
 
-  auto ds = std::make_unique<DeviceState>(
-      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
-  ds->device = d;
-  ds->shared_device = shared;
-  ds->rccl_ok = !shared;
-  ds->ipc_ok = ok && (!cfg_.ipc_selftest || ipc_selftest(*ds));
+  ds.recs = recs;
+  ds.shared_device = shared;
+  ds.rccl_ok = !shared;
+  if (!ok) {
+    ds.ipc_ok = false;
+  } else if (!cfg_.ipc_selftest) {
+    ds.ipc_ok = true;
+  } else if (all_cached) {
+    ds.ipc_ok = cached == '1';  // an earlier group with these members tested this topology
+  } else {
+    ds.ipc_ok = ipc_selftest(ds);
+    std::lock_guard<std::mutex> lk(g_verdict_mu);
+    g_ipc_verdict[vkey] = ds.ipc_ok;
+  }
+  ds.topo = true;
   if (cfg_.log_level >= 1)
-    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d shared_device=%d\n", rank_, d, bus,
-            (int)ds->rccl_ok, (int)ds->ipc_ok, (int)shared);
-  DeviceState& ref = *ds;
-  devs_[d] = std::move(ds);
-  return ref;
+    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d shared_device=%d%s\n", rank_, d, bus,
+            (int)ds.rccl_ok, (int)ds.ipc_ok, (int)shared, all_cached ? " (cached IPC verdict)" : "");
 }
 
+RcclOpts ProcessGroupMI355X::rccl_opts() const {
+  RcclOpts o;
+  o.min_ctas = cfg_.rccl_min_ctas;
+  o.max_ctas = cfg_.rccl_max_ctas;
+  o.split_share = cfg_.rccl_split_share ? 1 : 0;
+  return o;
+}
+
+// The group's RCCL communicator (lazy, collective over the group). A group whose
+// members equal those of a live communicator on this device (every demo of the
+// reference builds new_group(range(size)), main.py:11,21,31,46,63,75) splits
+// from it instead of bootstrapping a new one. All ranks vote first, so a rank
+// that has no such parent (or a different one) sends everyone down the fresh path.
 RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
-  if (!ds.rccl) {
-    auto c = std::make_unique<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device, cfg_.rccl_min_ctas,
-                                        cfg_.rccl_max_ctas);
-    std::lock_guard<std::mutex> lk(init_mu_);
-    ds.rccl = std::move(c);
+  if (ds.rccl) return *ds.rccl;
+  const auto t0 = std::chrono::steady_clock::now();
+  const std::string mk = members_key_ + "@" + std::to_string(ds.device);
+  std::shared_ptr<RcclComm> c;
+  const char* how = "init";
+  if (cfg_.group_comm != 2) {
+    auto parent = rccl_registry_get(mk);
+    const std::string tag = parent ? parent->tag : std::string();
+    const auto all = store_allgather(store_, "pdcc/rccl_parent", rank_, size_, std::vector<uint8_t>(tag.begin(), tag.end()));
+    bool agree = !tag.empty();
+    for (const auto& v : all) agree = agree && std::string(v.begin(), v.end()) == tag;
+    if (agree) {
+      if (cfg_.group_comm == 1) {
+        c = parent;
+        how = "share";
+      } else {
+        c = std::make_shared<RcclComm>(*parent, rank_, rccl_opts());
+        c->tag = parent->tag;
+        how = "split";
+      }
+    }
   }
+  if (!c) {
+    c = std::make_shared<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device, rccl_opts());
+    c->tag = group_name_ + "#" + mk;
+  }
+  rccl_registry_put(mk, c);
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    ds.rccl = c;
+  }
+  record_setup(std::string("rccl_comm/") + how, t0);
+  if (cfg_.log_level >= 1 && rank_ == 0)
+    fprintf(stderr, "[pdcc r0] group '%s': RCCL communicator (%s) in %.1f ms\n", group_name_.c_str(), how,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return *ds.rccl;
+}
+
+// 2-rank communicator for send/recv with `peer`: only the two ranks take part
+// (ProcessGroupNCCL keeps one per pair the same way), so point-to-point between
+// two ranks of a larger group never waits for the others.
+RcclComm& ProcessGroupMI355X::rccl_pair(DeviceState& ds, int peer) {
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    auto it = ds.pair_rccl.find(peer);
+    if (it != ds.pair_rccl.end()) return *it->second;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
+  auto c = std::make_shared<RcclComm>(store_, "pdcc/p2p/" + std::to_string(lo) + ":" + std::to_string(hi),
+                                      rank_ == lo ? 0 : 1, 2, ds.device, RcclOpts());
+  record_setup("rccl_comm/pair", t0);
+  std::lock_guard<std::mutex> lk(init_mu_);
+  ds.pair_rccl[peer] = c;
+  return *c;
+}
+
+// Are this rank and `peer` on different GPUs of one host? From the group topology when a
+// collective already exchanged it, else through a pairwise store exchange.
+bool ProcessGroupMI355X::pair_on_distinct_devices(DeviceState& ds, int peer) {
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    if (ds.topo) return ds.recs[peer] != ds.recs[rank_];
+    auto it = ds.pair_distinct.find(peer);
+    if (it != ds.pair_distinct.end()) return it->second;
+  }
+  char bus[64] = {0};
+  PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, ds.device));
+  char host[256] = {0};
+  gethostname(host, sizeof(host) - 1);
+  const std::string rec = std::string(host) + "|" + bus;
+  const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
+  const std::string key = "pdcc/p2pdev/" + std::to_string(lo) + ":" + std::to_string(hi) + "/";
+  store_->set(key + std::to_string(rank_), std::vector<uint8_t>(rec.begin(), rec.end()));
+  const auto v = store_->get(key + std::to_string(peer));
+  const std::string other(v.begin(), v.end());
+  const bool same_host = other.substr(0, other.find('|')) == std::string(host);
+  const bool distinct = same_host && other != rec;
+  std::lock_guard<std::mutex> lk(init_mu_);
+  ds.pair_distinct[peer] = distinct;
+  return distinct;
 }
 
 IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
   if (!ds.ipc) {
-    auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging,
-                                       (uint64_t)timeout_.count(), ds.shared_device);
+    const uint64_t spin = (uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count()));
+    auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging, spin,
+                                       ds.shared_device);
     std::lock_guard<std::mutex> lk(init_mu_);
     ds.ipc = c;
   }
@@ -228,7 +448,7 @@ IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
 // communicator is built, after the checks): one failure on any rank (handle
 // export or mapping, spin timeout, wrong data) turns IPC off for the whole group,
 // so a topology the protocol does not work on falls back to RCCL (or the host
-// path) instead of hanging or corrupting data. Called from dev_state() with
+// path) instead of hanging or corrupting data. Called from init_topology() with
 // init_mu_ held, on the group's comm stream (never a capturing one).
 bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
   auto vote = [&](const std::string& key, bool mine) {
@@ -304,7 +524,7 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
     ds.ipc.reset();  // every rank voted after its own kernels finished: nothing touches these buffers any more
     return false;
   }
-  ds.ipc->set_timeout_ms((uint64_t)timeout_.count());
+  ds.ipc->set_timeout_ms((uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count())));
   return true;
 }
 
@@ -443,80 +663,154 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   return w;
 }
 
-// =================================================================== all-reduce / reduce
-c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, RedOpType op, int root, bool rooted,
-                                                                 std::chrono::milliseconds to) {
-  const Coll cname = rooted ? Coll::REDUCE : Coll::ALLREDUCE;
-  TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
-  DeviceState& ds = dev_state(t);
-  const auto t0 = std::chrono::steady_clock::now();
-  const size_t bytes = t.nbytes();
-  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
-    record(cname, "local", bytes, t0);
-    return cpu_done(cname, {t});
-  }
-  kern::DType kd;
-  kern::RedOp ko;
-  const bool kok = kern_dtype(t.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
-  ncclDataType_t nd;
-  ncclRedOp_t no;
-  const bool nok = nccl_dtype(t.scalar_type(), nd) && nccl_op(op, t.scalar_type(), no);
-  const Algo a0 = choose(cname, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
-  if (a0 == Algo::HOST) {
-    at::Tensor h = t.cpu();
-    if (rooted) shm().reduce(h.data_ptr(), h.numel(), h.scalar_type(), op, root, to);
-    else shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
-    if (!rooted || rank_ == root) t.copy_(h);
-    record(cname, "host", bytes, t0);
-    return cpu_done(cname, {t});
-  }
-  at::Tensor w = prep_in(t);
-  Algo a2 = a0;
-  if (!rooted && !coalescing_) {
-    const auto cands = tune_candidates(cname, bytes, ds.rccl_ok && nok, ds.ipc_ok && kok);
-    if (!cands.empty()) {
-      a2 = tuned(cname, bytes);
-      const bool cap = capturing_on(ds.device);
-      if (a2 == Algo::AUTO && cap) a2 = a0;         // no timing runs inside a graph capture: static choice
-      if (a2 == Algo::HOST && cap) a2 = Algo::IPC;  // tuned to the host engine, which cannot be captured
-      if (a2 == Algo::AUTO) {
-        c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
-        const hipStream_t cs = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device).stream();
-        std::vector<at::Tensor> scratch;
-        for (size_t k = 0; k < cands.size(); ++k) scratch.push_back(w.clone(at::MemoryFormat::Contiguous));
-        a2 = autotune(
-            cname, bytes, ds, cands,
-            [&](size_t k) { enqueue_allreduce(cands[k], scratch[k], kd, ko, nd, no, op, root, false, ds, cs, to); },
-            [&](size_t r, size_t k) { return results_match(scratch[r], scratch[k], op, size_); });
-      }
-    }
-  }
-  const Algo a = a2;
-  if (a == Algo::HOST) {
-    // tuned to the host transport (small messages on groups without RCCL)
-    at::Tensor h = t.cpu();
-    shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
-    t.copy_(h);
-    record(cname, "host", bytes, t0);
-    return cpu_done(cname, {t});
-  }
-  std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
-    ipc(ds);
-    icp = ds.ipc;
-  }
-  const bool one_shot = bytes <= cfg_.ipc_1shot_max;
-  auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    enqueue_allreduce(a, w, kd, ko, nd, no, op, root, rooted, ds, s, to);
-    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
-  }, icp);
-  record(cname, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
-  return work;
+// =================================================================== autotuner
+std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const {
+  std::vector<Algo> v;
+  if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || !ipc_can || !same_host_ || coalescing_) return v;
+  if ((int)c >= 32 || !(cfg_.autotune_colls & (1u << (int)c))) return v;
+  if (bytes < cfg_.autotune_min || bytes > cfg_.autotune_max) return v;
+  if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
+  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
+  else return {};
+  v.push_back(Algo::IPC);
+  return v;
 }
 
+Algo ProcessGroupMI355X::tuned(const TuneKey& k) {
+  std::lock_guard<std::mutex> lk(tune_mu_);
+  auto it = tune_.find(k);
+  return it == tune_.end() ? Algo::AUTO : it->second.algo;
+}
+
+// The engine for one call. A decision for this key is used only if that engine is a
+// candidate of this call too; everything here depends on group-wide facts only
+// (topology, dtype/op support, the consensus table), so every rank picks the same.
+Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can,
+                                bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
+  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can);
+  if (cands.empty()) return a0;
+  const TuneKey key{(int)c, dtype, op, size_bucket(bytes)};
+  const Algo t = tuned(key);
+  const bool cap = capturing_on(ds.device);
+  if (t != Algo::AUTO) {
+    if (std::find(cands.begin(), cands.end(), t) == cands.end()) return a0;
+    if (t == Algo::HOST && cap) return Algo::IPC;  // tuned to the host engine, which cannot be captured
+    return t;
+  }
+  if (cap) return a0;  // no timing runs inside a graph capture: static choice
+  // every engine of the race exists before the clock starts (communicator setup is not timed)
+  for (Algo a : cands) {
+    if (a == Algo::RCCL) rccl(ds);
+    if (a == Algo::IPC) ipc(ds);
+  }
+  return tune(key, cands);
+}
+
+Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
+                                  const std::function<void(size_t)>& run,
+                                  const std::function<bool(size_t, size_t)>& same) {
+  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
+  const hipStream_t s = current_stream(ds.device);
+  const size_t n = cands.size();
+  auto elapsed_us = [](hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    PDCC_HIP(hipEventElapsedTime(&ms, a, b));
+    return 1e3 * (double)ms;
+  };
+  // 0) warm-up: one run each (staging growth, first-touch), then check every result
+  //    against the reference engine's on identical data
+  for (size_t k = 0; k < n; ++k) run(k);
+  PDCC_HIP(hipStreamSynchronize(s));
+  std::vector<double> v(2 * n, 0.0);  // [estimate_us x n, mismatch x n], MAX-reduced across ranks
+  for (size_t k = 1; k < n; ++k) v[n + k] = same(0, k) ? 0.0 : 1.0;
+  // 1) one timed run each: sizes the measurement (same count on every rank: MAX-reduced inputs)
+  std::vector<hipEvent_t> e1(n + 1);
+  for (auto& e : e1) PDCC_HIP(hipEventCreate(&e));
+  PDCC_HIP(hipEventRecord(e1[0], s));
+  for (size_t k = 0; k < n; ++k) {
+    run(k);
+    PDCC_HIP(hipEventRecord(e1[k + 1], s));
+  }
+  PDCC_HIP(hipEventSynchronize(e1[n]));
+  for (size_t k = 0; k < n; ++k) v[k] = elapsed_us(e1[k], e1[k + 1]);
+  for (auto& e : e1) hipEventDestroy(e);
+  shm().allreduce(v.data(), v.size(), at::kDouble, RedOpType::MAX, timeout_);
+  double slow = 1.0;
+  for (size_t k = 0; k < n; ++k) slow = std::max(slow, v[k]);
+  const int iters = (int)std::max(3.0, std::min(25.0, std::ceil(30000.0 / slow)));
+  // 2) interleaved timed runs (ref, ipc, ref, ipc, ...): drift hits both engines alike
+  std::vector<hipEvent_t> ev(iters * n + 1);
+  for (auto& e : ev) PDCC_HIP(hipEventCreate(&e));
+  PDCC_HIP(hipEventRecord(ev[0], s));
+  for (int i = 0; i < iters; ++i)
+    for (size_t k = 0; k < n; ++k) {
+      run(k);
+      PDCC_HIP(hipEventRecord(ev[i * n + k + 1], s));
+    }
+  PDCC_HIP(hipEventSynchronize(ev[iters * n]));
+  std::vector<double> med(n);
+  for (size_t k = 0; k < n; ++k) {
+    std::vector<double> t;
+    for (int i = 0; i < iters; ++i) t.push_back(elapsed_us(ev[i * n + k], ev[i * n + k + 1]));
+    std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
+    med[k] = t[t.size() / 2];
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  // 3) every rank adopts the same engine: slowest rank's median, any rank's mismatch
+  shm().allreduce(med.data(), med.size(), at::kDouble, RedOpType::MAX, timeout_);
+  size_t best = 0;
+  for (size_t k = 1; k < n; ++k)
+    if (v[n + k] == 0.0 && med[k] < med[best]) best = k;
+  TuneEntry te;
+  te.ref = cands[0];
+  te.iters = iters;
+  for (size_t k = 0; k < n; ++k) {
+    if (cands[k] == Algo::IPC) {
+      te.ipc_us = med[k];
+      te.valid = v[n + k] == 0.0;
+    } else {
+      te.rccl_us = med[k];  // the reference engine (RCCL, or the host transport without RCCL)
+    }
+  }
+  te.algo = cands[best];
+  {
+    std::lock_guard<std::mutex> lk(tune_mu_);
+    tune_[key] = te;
+  }
+  if (cfg_.log_level >= 1 && rank_ == 0)
+    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us%s (%d runs each) -> %s\n",
+            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.ipc_us,
+            te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
+  return te.algo;
+}
+
+std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table() {
+  std::lock_guard<std::mutex> lk(tune_mu_);
+  std::vector<TuneRecord> out;
+  for (const auto& kv : tune_) {
+    const TuneEntry& e = kv.second;
+    const int dt = std::get<1>(kv.first), op = std::get<2>(kv.first), b = std::get<3>(kv.first);
+    TuneRecord r;
+    r.coll = coll_name((Coll)std::get<0>(kv.first));
+    r.dtype = dt < 0 ? "-" : c10::toString((at::ScalarType)dt);
+    r.op = op == kLayoutFlat ? "flat" : op == kLayoutList ? "list" : op < 0 ? "-" : op_name(op);
+    r.lo = 1ull << b;
+    r.hi = 2ull << b;
+    r.ref = algo_name(e.ref);
+    r.rccl_us = e.rccl_us;
+    r.ipc_us = e.ipc_us;
+    r.valid = e.valid;
+    r.algo = algo_name(e.algo);
+    r.iters = e.iters;
+    out.push_back(r);
+  }
+  return out;
+}
+
+// =================================================================== engines
 void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko,
-                                           ncclDataType_t nd, ncclRedOp_t no, RedOpType op, int root, bool rooted,
-                                           DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+                                           ncclDataType_t nd, ncclRedOp_t no, bool nok, RedOpType op, int root,
+                                           bool rooted, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
   if (a == Algo::IPC) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -532,141 +826,331 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     c.out[0] = w.data_ptr();
     ipc_chunked(ic, c, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
+    TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
     RcclComm& rc = rccl(ds);
     if (rooted) PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
     else PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
-  } else {  // HOST, synchronous (autotuner candidate)
+  } else {  // HOST, synchronous
     PDCC_HIP(hipStreamSynchronize(s));
     at::Tensor h = w.cpu();
     if (rooted) shm().reduce(h.data_ptr(), h.numel(), h.scalar_type(), op, root, to);
     else shm().allreduce(h.data_ptr(), h.numel(), h.scalar_type(), op, to);
-    const_cast<at::Tensor&>(w).copy_(h);
+    if (!rooted || rank_ == root) const_cast<at::Tensor&>(w).copy_(h);
   }
 }
 
-// =================================================================== autotuner
-std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const {
-  std::vector<Algo> v;
-  if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || c != Coll::ALLREDUCE || !ipc_can || !same_host_) return v;
-  if (bytes < cfg_.autotune_min || bytes > cfg_.autotune_max) return v;
-  if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
-  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
-  else return {};
-  v.push_back(Algo::IPC);
-  return v;
+void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root, DeviceState& ds, hipStream_t s,
+                                           std::chrono::milliseconds to) {
+  const size_t bytes = w.nbytes();
+  if (a == Algo::IPC) {
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    c.coll = bytes <= cfg_.ipc_1shot_max ? kern::IpcColl::BROADCAST_1SHOT : kern::IpcColl::BROADCAST_2SHOT;
+    c.dtype = kern::DType::U8;
+    c.op = kern::RedOp::COPY;
+    c.root = root;
+    c.bytes = bytes;
+    c.in[0] = w.data_ptr();
+    c.out[0] = w.data_ptr();
+    ipc_chunked(ic, c, ic.max_staging(), s);
+  } else if (a == Algo::RCCL) {
+    PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rccl(ds).get(), s));
+  } else {
+    PDCC_HIP(hipStreamSynchronize(s));
+    at::Tensor h = w.cpu();
+    shm().broadcast(h.data_ptr(), bytes, root, to);
+    if (rank_ != root) const_cast<at::Tensor&>(w).copy_(h);
+  }
 }
 
-Algo ProcessGroupMI355X::tuned(Coll c, size_t bytes) {
-  std::lock_guard<std::mutex> lk(tune_mu_);
-  auto it = tune_.find({(int)c, size_bucket(bytes)});
-  return it == tune_.end() ? Algo::AUTO : it->second.algo;
-}
-
-Algo ProcessGroupMI355X::autotune(Coll c, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
-                                  const std::function<void(size_t)>& run,
-                                  const std::function<bool(size_t, size_t)>& same) {
-  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
-  const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device).stream();
-  const size_t n = cands.size();
-  // 1) one run each on identical copies of the caller's data, then compare with the reference
-  for (size_t k = 0; k < n; ++k) run(k);
-  PDCC_HIP(hipStreamSynchronize(s));
-  std::vector<double> v(2 * n, 0.0);  // [time_us x n, mismatch x n], MAX-reduced across ranks
-  for (size_t k = 1; k < n; ++k) v[n + k] = same(0, k) ? 0.0 : 1.0;
-  // 2) time `iters` back-to-back runs of each engine with events on the caller's stream
-  const int iters = bytes >= (64u << 20) ? 3 : bytes >= (1u << 20) ? 10 : 30;
-  std::vector<hipEvent_t> ev(n + 1);
-  for (auto& e : ev) PDCC_HIP(hipEventCreate(&e));
-  PDCC_HIP(hipEventRecord(ev[0], s));
-  for (size_t k = 0; k < n; ++k) {
-    for (int i = 0; i < iters; ++i) run(k);
-    PDCC_HIP(hipEventRecord(ev[k + 1], s));
-  }
-  PDCC_HIP(hipEventSynchronize(ev[n]));
-  for (size_t k = 0; k < n; ++k) {
-    float ms = 0.f;
-    PDCC_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-    v[k] = 1e3 * ms / iters;
-  }
-  for (auto& e : ev) hipEventDestroy(e);
-  // 3) every rank adopts the same engine: slowest rank's time, any rank's mismatch
-  shm().allreduce(v.data(), v.size(), at::kDouble, RedOpType::MAX, timeout_);
-  size_t best = 0;
-  for (size_t k = 1; k < n; ++k)
-    if (v[n + k] == 0.0 && v[k] < v[best]) best = k;
-  TuneEntry te;
-  for (size_t k = 0; k < n; ++k) {
-    if (cands[k] == Algo::IPC) {
-      te.ipc_us = v[k];
-      te.valid = v[n + k] == 0.0;
+void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const std::vector<at::Tensor>& wo, int root,
+                                           bool rooted, DeviceState& ds, hipStream_t s,
+                                           std::chrono::milliseconds to) {
+  const size_t bytes = wi.nbytes();
+  const bool receiver = !rooted || rank_ == root;
+  if (a == Algo::IPC) {
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    c.coll = rooted ? kern::IpcColl::GATHER : kern::IpcColl::ALLGATHER;
+    c.dtype = kern::DType::U8;
+    c.op = kern::RedOp::COPY;
+    c.root = root;
+    c.bytes = bytes;
+    c.in[0] = wi.data_ptr();
+    if (receiver)
+      for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
+    ipc_chunked(ic, c, ic.max_staging(), s);
+  } else if (a == Algo::RCCL) {
+    RcclComm& rc = rccl(ds);
+    if (!rooted && is_flat(wo, bytes)) {
+      PDCC_NCCL(ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc.get(), s));
+    } else if (!rooted && !cfg_.list_gather_p2p) {
+      // staged: one ring all-gather into a staging buffer, then K2 unpacks into the list
+      at::Tensor stg = at::empty({(int64_t)(bytes * size_)}, wi.options().dtype(at::kByte));
+      PDCC_NCCL(ncclAllGather(wi.data_ptr(), stg.data_ptr(), bytes, ncclUint8, rc.get(), s));
+      std::vector<kern::CopyDesc> d;
+      for (int r = 0; r < size_; ++r)
+        d.push_back({static_cast<char*>(stg.data_ptr()) + r * bytes, wo[r].data_ptr(), bytes});
+      multi_copy_or_memcpy(d, s);
     } else {
-      te.rccl_us = v[k];  // the reference engine (RCCL, or the host transport without RCCL)
+      // zero copy: every receiver posts one recv per peer straight into its list entry;
+      // over a fully connected xGMI node the W-1 transfers of a rank use W-1 links at once
+      PDCC_NCCL(ncclGroupStart());
+      for (int r = 0; r < size_; ++r) {
+        if (r == rank_) continue;
+        if (!rooted || r == root) PDCC_NCCL(ncclSend(wi.data_ptr(), bytes, ncclUint8, r, rc.get(), s));
+        if (receiver) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), bytes, ncclUint8, r, rc.get(), s));
+      }
+      PDCC_NCCL(ncclGroupEnd());
+      if (receiver && bytes)
+        PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi.data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
     }
+  } else {
+    PDCC_HIP(hipStreamSynchronize(s));
+    at::Tensor h = wi.cpu();
+    std::vector<at::Tensor> ho;
+    std::vector<void*> ptrs(size_, nullptr);
+    if (receiver)
+      for (int r = 0; r < size_; ++r) {
+        ho.push_back(at::empty_like(h));
+        ptrs[r] = ho.back().data_ptr();
+      }
+    if (rooted) shm().gather(h.data_ptr(), ptrs, bytes, root, to);
+    else shm().allgather(h.data_ptr(), ptrs, bytes, to);
+    if (receiver)
+      for (int r = 0; r < size_; ++r) const_cast<at::Tensor&>(wo[r]).copy_(ho[r]);
   }
-  te.algo = cands[best];
-  {
-    std::lock_guard<std::mutex> lk(tune_mu_);
-    tune_[{(int)c, size_bucket(bytes)}] = te;
-  }
-  if (cfg_.log_level >= 1 && rank_ == 0)
-    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us%s -> %s\n", coll_name(c), bytes,
-            cands[0] == Algo::RCCL ? "rccl" : "host", te.rccl_us, te.ipc_us, te.valid ? "" : " (MISMATCH)",
-            te.algo == Algo::IPC ? "ipc" : (te.algo == Algo::RCCL ? "rccl" : "host"));
-  return te.algo;
 }
 
-std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table() {
-  std::lock_guard<std::mutex> lk(tune_mu_);
-  std::vector<TuneRecord> out;
-  for (const auto& kv : tune_) {
-    const TuneEntry& e = kv.second;
-    out.push_back({coll_name((Coll)kv.first.first), 1ull << kv.first.second, 2ull << kv.first.second, e.rccl_us,
-                   e.ipc_us, e.valid,
-                   e.algo == Algo::IPC ? "ipc" : (e.algo == Algo::RCCL ? "rccl" : "host")});
+void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& wi, const at::Tensor& wo, int root,
+                                         DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+  const size_t bytes = wo.nbytes();
+  if (a == Algo::IPC) {
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    c.coll = kern::IpcColl::SCATTER;
+    c.dtype = kern::DType::U8;
+    c.op = kern::RedOp::COPY;
+    c.root = root;
+    c.bytes = bytes;
+    if (rank_ == root)
+      for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
+    c.out[0] = wo.data_ptr();
+    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+  } else if (a == Algo::RCCL) {
+    RcclComm& rc = rccl(ds);
+    PDCC_NCCL(ncclGroupStart());
+    if (rank_ == root) {
+      for (int r = 0; r < size_; ++r)
+        if (r != root) PDCC_NCCL(ncclSend(wi[r].data_ptr(), bytes, ncclUint8, r, rc.get(), s));
+    } else {
+      PDCC_NCCL(ncclRecv(wo.data_ptr(), bytes, ncclUint8, root, rc.get(), s));
+    }
+    PDCC_NCCL(ncclGroupEnd());
+    if (rank_ == root && bytes)
+      PDCC_HIP(hipMemcpyAsync(wo.data_ptr(), wi[root].data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
+  } else {
+    PDCC_HIP(hipStreamSynchronize(s));
+    std::vector<at::Tensor> hi;
+    std::vector<const void*> ptrs(size_, nullptr);
+    if (rank_ == root)
+      for (int r = 0; r < size_; ++r) {
+        hi.push_back(wi[r].cpu().contiguous());
+        ptrs[r] = hi.back().data_ptr();
+      }
+    at::Tensor h = at::empty(wo.sizes(), wo.options().device(at::kCPU));
+    shm().scatter(ptrs, h.data_ptr(), bytes, root, to);
+    const_cast<at::Tensor&>(wo).copy_(h);
   }
-  return out;
+}
+
+void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Tensor>& wi, const at::Tensor& wo,
+                                                kern::DType kd, kern::RedOp ko, ncclDataType_t nd, ncclRedOp_t no,
+                                                bool nok, RedOpType op, DeviceState& ds, hipStream_t s,
+                                                std::chrono::milliseconds to) {
+  const size_t bytes = wo.nbytes();
+  if (a == Algo::IPC) {
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    c.coll = kern::IpcColl::REDUCE_SCATTER;
+    c.dtype = kd;
+    c.op = ko;
+    c.avg_div = size_;
+    c.bytes = bytes;
+    for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
+    c.out[0] = wo.data_ptr();
+    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+  } else if (a == Algo::RCCL) {
+    TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", wo.scalar_type());
+    RcclComm& rc = rccl(ds);
+    const void* src;
+    at::Tensor stg;
+    if (is_flat(wi, bytes)) {
+      src = wi[0].data_ptr();
+    } else {  // K2 pack into one staging buffer
+      stg = at::empty({(int64_t)(bytes * size_)}, wo.options().dtype(at::kByte));
+      std::vector<kern::CopyDesc> d;
+      for (int r = 0; r < size_; ++r)
+        d.push_back({wi[r].data_ptr(), static_cast<char*>(stg.data_ptr()) + r * bytes, bytes});
+      multi_copy_or_memcpy(d, s);
+      src = stg.data_ptr();
+    }
+    PDCC_NCCL(ncclReduceScatter(src, wo.data_ptr(), wo.numel(), nd, no, rc.get(), s));
+  } else {
+    PDCC_HIP(hipStreamSynchronize(s));
+    std::vector<at::Tensor> hi;
+    std::vector<const void*> ptrs;
+    for (const auto& i : wi) {
+      hi.push_back(i.cpu().contiguous());
+      ptrs.push_back(hi.back().data_ptr());
+    }
+    at::Tensor h = at::empty(wo.sizes(), wo.options().device(at::kCPU));
+    shm().reduce_scatter(ptrs, h.data_ptr(), wo.numel(), wo.scalar_type(), op, to);
+    const_cast<at::Tensor&>(wo).copy_(h);
+  }
+}
+
+void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>& wi, const std::vector<at::Tensor>& wo,
+                                          bool equal, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+  if (a == Algo::IPC) {
+    TORCH_CHECK(equal, "pdcc: the IPC all-to-all needs equal splits");
+    IpcComm& ic = ipc(ds);
+    kern::IpcCall c{};
+    c.coll = kern::IpcColl::ALLTOALL;
+    c.dtype = kern::DType::U8;
+    c.op = kern::RedOp::COPY;
+    c.bytes = wi[0].nbytes();
+    for (int r = 0; r < size_; ++r) {
+      c.in[r] = wi[r].data_ptr();
+      c.out[r] = wo[r].data_ptr();
+    }
+    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+  } else if (a == Algo::RCCL) {
+    RcclComm& rc = rccl(ds);
+    const size_t chunk = wi[0].nbytes();
+    if (equal && is_flat(wi, chunk) && is_flat(wo, chunk)) {
+      PDCC_NCCL(ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc.get(), s));
+    } else {
+      PDCC_NCCL(ncclGroupStart());
+      for (int r = 0; r < size_; ++r) {
+        if (r == rank_) continue;
+        if (wi[r].nbytes()) PDCC_NCCL(ncclSend(wi[r].data_ptr(), wi[r].nbytes(), ncclUint8, r, rc.get(), s));
+        if (wo[r].nbytes()) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), wo[r].nbytes(), ncclUint8, r, rc.get(), s));
+      }
+      PDCC_NCCL(ncclGroupEnd());
+      if (wi[rank_].nbytes())
+        PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi[rank_].data_ptr(), wi[rank_].nbytes(),
+                                hipMemcpyDeviceToDevice, s));
+    }
+  } else {
+    PDCC_HIP(hipStreamSynchronize(s));
+    std::vector<at::Tensor> hi, ho;
+    std::vector<const void*> ip;
+    std::vector<void*> op;
+    std::vector<size_t> sb, rb;
+    for (const auto& i : wi) {
+      hi.push_back(i.cpu().contiguous());
+      ip.push_back(hi.back().data_ptr());
+      sb.push_back(hi.back().nbytes());
+    }
+    for (const auto& o : wo) {
+      ho.push_back(at::empty(o.sizes(), o.options().device(at::kCPU)));
+      op.push_back(ho.back().data_ptr());
+      rb.push_back(ho.back().nbytes());
+    }
+    shm().alltoall(ip, sb, op, rb, to);
+    for (size_t i = 0; i < wo.size(); ++i) const_cast<at::Tensor&>(wo[i]).copy_(ho[i]);
+  }
+}
+
+// =================================================================== all-reduce / reduce
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, RedOpType op, int root, bool rooted,
+                                                                 std::chrono::milliseconds to) {
+  const Coll cname = rooted ? Coll::REDUCE : Coll::ALLREDUCE;
+  TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t bytes = t.nbytes();
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    record(cname, "local", bytes, t0);
+    return cpu_done(cname, {t});
+  }
+  DeviceState& ds = dev_state(t);
+  kern::DType kd;
+  kern::RedOp ko;
+  const bool kok = kern_dtype(t.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
+  ncclDataType_t nd = ncclFloat32;
+  ncclRedOp_t no = ncclSum;
+  const bool nok = nccl_dtype(t.scalar_type(), nd) && nccl_op(op, t.scalar_type(), no);
+  const bool rccl_can = ds.rccl_ok && nok, ipc_can = ds.ipc_ok && kok;
+  const Algo a0 = choose(cname, bytes, ds, rccl_can, ipc_can);
+  at::Tensor w = prep_in(t);
+  const Algo a = decide(cname, (int)t.scalar_type(), (int)op, bytes, ds, a0, rccl_can, ipc_can,
+                        [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(w.numel(), w.element_size(), cfg_.autotune_sample);
+    std::vector<at::Tensor> sc;
+    for (size_t k = 0; k < cands.size(); ++k) sc.push_back(w.reshape({-1}).narrow(0, 0, n).clone());
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, bytes, ds, cands,
+        [&](size_t k) { enqueue_allreduce(cands[k], sc[k], kd, ko, nd, no, nok, op, root, rooted, ds, cs, to); },
+        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); });
+  });
+  if (a == Algo::HOST) {
+    enqueue_allreduce(Algo::HOST, w, kd, ko, nd, no, nok, op, root, rooted, ds, current_stream(ds.device), to);
+    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+    record(cname, "host", bytes, t0);
+    return cpu_done(cname, {t});
+  }
+  std::shared_ptr<IpcComm> icp;
+  if (a == Algo::IPC) {
+    ipc(ds);
+    icp = ds.ipc;
+  }
+  const bool one_shot = bytes <= cfg_.ipc_1shot_max;
+  auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
+    enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
+    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+  }, icp);
+  record(cname, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  return work;
 }
 
 // =================================================================== broadcast
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, int root,
                                                                  std::chrono::milliseconds to) {
-  DeviceState& ds = dev_state(t);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = t.nbytes();
   if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
     record(Coll::BROADCAST, "local", bytes, t0);
     return cpu_done(Coll::BROADCAST, {t});
   }
-  const Algo a = choose(Coll::BROADCAST, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  DeviceState& ds = dev_state(t);
+  const Algo a0 = choose(Coll::BROADCAST, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  at::Tensor w = prep_in(t);
+  const Algo a = decide(Coll::BROADCAST, -1, -1, bytes, ds, a0, ds.rccl_ok, ds.ipc_ok,
+                        [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(w.numel(), w.element_size(), cfg_.autotune_sample);
+    std::vector<at::Tensor> sc;
+    for (size_t k = 0; k < cands.size(); ++k) sc.push_back(w.reshape({-1}).narrow(0, 0, n).clone());
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, bytes, ds, cands, [&](size_t k) { enqueue_broadcast(cands[k], sc[k], root, ds, cs, to); },
+        [&](size_t r, size_t k) { return at::equal(sc[r], sc[k]); });
+  });
   if (a == Algo::HOST) {
-    at::Tensor h = t.cpu();
-    shm().broadcast(h.data_ptr(), h.nbytes(), root, to);
-    if (rank_ != root) t.copy_(h);
+    enqueue_broadcast(Algo::HOST, w, root, ds, current_stream(ds.device), to);
+    if (!w.is_same(t) && rank_ != root) t.copy_(w);
     record(Coll::BROADCAST, "host", bytes, t0);
     return cpu_done(Coll::BROADCAST, {t});
   }
-  at::Tensor w = prep_in(t);
   std::shared_ptr<IpcComm> icp;
   if (a == Algo::IPC) {
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
   auto work = gpu_run(Coll::BROADCAST, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = one_shot ? kern::IpcColl::BROADCAST_1SHOT : kern::IpcColl::BROADCAST_2SHOT;
-      c.dtype = kern::DType::U8;
-      c.op = kern::RedOp::COPY;
-      c.root = root;
-      c.bytes = bytes;
-      c.in[0] = w.data_ptr();
-      c.out[0] = w.data_ptr();
-      ipc_chunked(*icp, c, icp->max_staging(), s);
-    } else {
-      PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
-    }
+    enqueue_broadcast(a, w, root, ds, s, to);
     if (!w.is_same(t) && rank_ != root) t.copy_(w);
   }, icp);
   record(Coll::BROADCAST, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
@@ -678,36 +1162,43 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
                                                                  int root, bool rooted,
                                                                  std::chrono::milliseconds to) {
   const Coll cname = rooted ? Coll::GATHER : Coll::ALLGATHER;
-  DeviceState& ds = dev_state(in);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = in.nbytes();
   const bool receiver = !rooted || rank_ == root;
-  if (size_ == 1 && cfg_.world1_local) {
-    outs[0].copy_(in);
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    if (!outs.empty()) outs[0].copy_(in);
     record(cname, "local", bytes, t0);
     return cpu_done(cname, outs);
   }
-  const Algo a = choose(cname, bytes, ds, ds.rccl_ok, ds.ipc_ok);
-  if (a == Algo::HOST) {
-    at::Tensor h = in.cpu();
-    std::vector<at::Tensor> ho;
-    std::vector<void*> ptrs(size_, nullptr);
-    if (receiver)
-      for (int r = 0; r < size_; ++r) {
-        ho.push_back(at::empty_like(h));
-        ptrs[r] = ho.back().data_ptr();
-      }
-    if (rooted) shm().gather(h.data_ptr(), ptrs, bytes, root, to);
-    else shm().allgather(h.data_ptr(), ptrs, bytes, to);
-    if (receiver)
-      for (int r = 0; r < size_; ++r) outs[r].copy_(ho[r]);
-    record(cname, "host", bytes, t0);
-    return cpu_done(cname, outs);
-  }
+  DeviceState& ds = dev_state(in);
+  const Algo a0 = choose(cname, bytes, ds, ds.rccl_ok, ds.ipc_ok);
   at::Tensor wi = prep_in(in);
   std::vector<at::Tensor> wo;
   if (receiver)
     for (auto& o : outs) wo.push_back(prep_out(o));
+  // the layout is part of the key (RCCL takes a different path for a flat output);
+  // on gather only the root has outputs, so the key cannot depend on them there
+  const bool flat = !rooted && is_flat(wo, bytes);
+  const Algo a = decide(cname, -1, rooted ? -1 : (flat ? kLayoutFlat : kLayoutList), bytes, ds, a0, ds.rccl_ok,
+                        ds.ipc_ok, [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(wi.numel(), wi.element_size(), cfg_.autotune_sample, size_);
+    const at::Tensor si = wi.reshape({-1}).narrow(0, 0, n);
+    std::vector<std::vector<at::Tensor>> sc(cands.size());
+    if (receiver)
+      for (size_t k = 0; k < cands.size(); ++k) sc[k] = scratch_outputs(wi.options(), size_, n, flat);
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, bytes, ds, cands, [&](size_t k) { enqueue_allgather(cands[k], si, sc[k], root, rooted, ds, cs, to); },
+        [&](size_t r, size_t k) { return lists_equal(sc[r], sc[k]); });
+  });
+  if (a == Algo::HOST) {
+    enqueue_allgather(Algo::HOST, wi, wo, root, rooted, ds, current_stream(ds.device), to);
+    if (receiver)
+      for (int r = 0; r < size_; ++r)
+        if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+    record(cname, "host", bytes, t0);
+    return cpu_done(cname, outs);
+  }
   std::vector<at::Tensor> keep{in, wi};
   for (auto& o : wo) keep.push_back(o);
   std::shared_ptr<IpcComm> icp;
@@ -715,41 +1206,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
-  const char* algo = a == Algo::IPC ? "ipc" : "rccl";
+  const char* algo = a == Algo::IPC ? "ipc" : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
   auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = rooted ? kern::IpcColl::GATHER : kern::IpcColl::ALLGATHER;
-      c.dtype = kern::DType::U8;
-      c.op = kern::RedOp::COPY;
-      c.root = root;
-      c.bytes = bytes;
-      c.in[0] = wi.data_ptr();
-      if (receiver)
-        for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
-      ipc_chunked(*icp, c, icp->max_staging(), s);
-    } else if (!rooted) {
-      if (is_flat(wo, bytes)) {
-        PDCC_NCCL(ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc->get(), s));
-      } else {
-        at::Tensor stg = at::empty({(int64_t)(bytes * size_)}, in.options().dtype(at::kByte));
-        PDCC_NCCL(ncclAllGather(wi.data_ptr(), stg.data_ptr(), bytes, ncclUint8, rc->get(), s));
-        std::vector<kern::CopyDesc> d;
-        for (int r = 0; r < size_; ++r) d.push_back({static_cast<char*>(stg.data_ptr()) + r * bytes, wo[r].data_ptr(), bytes});
-        multi_copy_or_memcpy(d, s);  // K2 unpack
-      }
-    } else {
-      PDCC_NCCL(ncclGroupStart());
-      if (rank_ == root) {
-        for (int r = 0; r < size_; ++r)
-          if (r != root) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), bytes, ncclUint8, r, rc->get(), s));
-      } else {
-        PDCC_NCCL(ncclSend(wi.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
-      }
-      PDCC_NCCL(ncclGroupEnd());
-      if (rank_ == root) PDCC_HIP(hipMemcpyAsync(wo[root].data_ptr(), wi.data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
-    }
+    enqueue_allgather(a, wi, wo, root, rooted, ds, s, to);
     if (receiver)
       for (int r = 0; r < size_; ++r)
         if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
@@ -761,33 +1220,36 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
 // =================================================================== scatter
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
                                                                int root, std::chrono::milliseconds to) {
-  DeviceState& ds = dev_state(out);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = out.nbytes();
-  if (size_ == 1 && cfg_.world1_local) {
-    out.copy_(ins[0]);
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    if (!ins.empty()) out.copy_(ins[0]);
     record(Coll::SCATTER, "local", bytes, t0);
     return cpu_done(Coll::SCATTER, {out});
   }
-  const Algo a = choose(Coll::SCATTER, bytes, ds, ds.rccl_ok, ds.ipc_ok);
-  if (a == Algo::HOST) {
-    std::vector<at::Tensor> hi;
-    std::vector<const void*> ptrs(size_, nullptr);
-    if (rank_ == root)
-      for (int r = 0; r < size_; ++r) {
-        hi.push_back(ins[r].cpu().contiguous());
-        ptrs[r] = hi.back().data_ptr();
-      }
-    at::Tensor h = at::empty(out.sizes(), out.options().device(at::kCPU));
-    shm().scatter(ptrs, h.data_ptr(), bytes, root, to);
-    out.copy_(h);
-    record(Coll::SCATTER, "host", bytes, t0);
-    return cpu_done(Coll::SCATTER, {out});
-  }
+  DeviceState& ds = dev_state(out);
+  const Algo a0 = choose(Coll::SCATTER, bytes, ds, ds.rccl_ok, ds.ipc_ok);
   std::vector<at::Tensor> wi;
   if (rank_ == root)
     for (auto& i : ins) wi.push_back(prep_in(i));
   at::Tensor wo = prep_out(out);
+  const Algo a = decide(Coll::SCATTER, -1, -1, bytes, ds, a0, ds.rccl_ok, ds.ipc_ok,
+                        [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(wo.numel(), wo.element_size(), cfg_.autotune_sample, size_);
+    const std::vector<at::Tensor> si = sample_inputs(wi, n, false);
+    std::vector<at::Tensor> sc;
+    for (size_t k = 0; k < cands.size(); ++k) sc.push_back(at::empty({n}, wo.options()));
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, bytes, ds, cands, [&](size_t k) { enqueue_scatter(cands[k], si, sc[k], root, ds, cs, to); },
+        [&](size_t r, size_t k) { return at::equal(sc[r], sc[k]); });
+  });
+  if (a == Algo::HOST) {
+    enqueue_scatter(Algo::HOST, wi, wo, root, ds, current_stream(ds.device), to);
+    if (!wo.is_same(out)) out.copy_(wo);
+    record(Coll::SCATTER, "host", bytes, t0);
+    return cpu_done(Coll::SCATTER, {out});
+  }
   std::vector<at::Tensor> keep{out, wo};
   for (auto& i : wi) keep.push_back(i);
   std::shared_ptr<IpcComm> icp;
@@ -795,30 +1257,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
   auto work = gpu_run(Coll::SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = kern::IpcColl::SCATTER;
-      c.dtype = kern::DType::U8;
-      c.op = kern::RedOp::COPY;
-      c.root = root;
-      c.bytes = bytes;
-      if (rank_ == root)
-        for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
-      c.out[0] = wo.data_ptr();
-      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
-    } else {
-      PDCC_NCCL(ncclGroupStart());
-      if (rank_ == root) {
-        for (int r = 0; r < size_; ++r)
-          if (r != root) PDCC_NCCL(ncclSend(wi[r].data_ptr(), bytes, ncclUint8, r, rc->get(), s));
-      } else {
-        PDCC_NCCL(ncclRecv(wo.data_ptr(), bytes, ncclUint8, root, rc->get(), s));
-      }
-      PDCC_NCCL(ncclGroupEnd());
-      if (rank_ == root) PDCC_HIP(hipMemcpyAsync(wo.data_ptr(), wi[root].data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
-    }
+    enqueue_scatter(a, wi, wo, root, ds, s, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
   record(Coll::SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
@@ -829,37 +1269,43 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
                                                                       RedOpType op, std::chrono::milliseconds to) {
   TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
-  DeviceState& ds = dev_state(out);
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = out.nbytes();
-  if (size_ == 1 && cfg_.world1_local) {
-    out.copy_(ins[0]);
+  if ((size_ == 1 && cfg_.world1_local) || bytes == 0) {
+    if (!ins.empty()) out.copy_(ins[0]);
     record(Coll::REDUCE_SCATTER, "local", bytes, t0);
     return cpu_done(Coll::REDUCE_SCATTER, {out});
   }
+  DeviceState& ds = dev_state(out);
   kern::DType kd;
   kern::RedOp ko;
   const bool kok = kern_dtype(out.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
-  ncclDataType_t nd;
-  ncclRedOp_t no;
+  ncclDataType_t nd = ncclFloat32;
+  ncclRedOp_t no = ncclSum;
   const bool nok = nccl_dtype(out.scalar_type(), nd) && nccl_op(op, out.scalar_type(), no);
-  const Algo a = choose(Coll::REDUCE_SCATTER, bytes, ds, ds.rccl_ok && nok, ds.ipc_ok && kok);
-  if (a == Algo::HOST) {
-    std::vector<at::Tensor> hi;
-    std::vector<const void*> ptrs;
-    for (auto& i : ins) {
-      hi.push_back(i.cpu().contiguous());
-      ptrs.push_back(hi.back().data_ptr());
-    }
-    at::Tensor h = at::empty(out.sizes(), out.options().device(at::kCPU));
-    shm().reduce_scatter(ptrs, h.data_ptr(), out.numel(), out.scalar_type(), op, to);
-    out.copy_(h);
-    record(Coll::REDUCE_SCATTER, "host", bytes, t0);
-    return cpu_done(Coll::REDUCE_SCATTER, {out});
-  }
+  const bool rccl_can = ds.rccl_ok && nok, ipc_can = ds.ipc_ok && kok;
+  const Algo a0 = choose(Coll::REDUCE_SCATTER, bytes, ds, rccl_can, ipc_can);
   std::vector<at::Tensor> wi;
   for (auto& i : ins) wi.push_back(prep_in(i));
   at::Tensor wo = prep_out(out);
+  const Algo a = decide(Coll::REDUCE_SCATTER, (int)out.scalar_type(), (int)op, bytes, ds, a0, rccl_can, ipc_can,
+                        [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(wo.numel(), wo.element_size(), cfg_.autotune_sample, size_);
+    const std::vector<at::Tensor> si = sample_inputs(wi, n, is_flat(wi, bytes));
+    std::vector<at::Tensor> sc;
+    for (size_t k = 0; k < cands.size(); ++k) sc.push_back(at::empty({n}, wo.options()));
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, bytes, ds, cands,
+        [&](size_t k) { enqueue_reduce_scatter(cands[k], si, sc[k], kd, ko, nd, no, nok, op, ds, cs, to); },
+        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); });
+  });
+  if (a == Algo::HOST) {
+    enqueue_reduce_scatter(Algo::HOST, wi, wo, kd, ko, nd, no, nok, op, ds, current_stream(ds.device), to);
+    if (!wo.is_same(out)) out.copy_(wo);
+    record(Coll::REDUCE_SCATTER, "host", bytes, t0);
+    return cpu_done(Coll::REDUCE_SCATTER, {out});
+  }
   std::vector<at::Tensor> keep{out, wo};
   for (auto& i : wi) keep.push_back(i);
   std::shared_ptr<IpcComm> icp;
@@ -867,32 +1313,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
   auto work = gpu_run(Coll::REDUCE_SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = kern::IpcColl::REDUCE_SCATTER;
-      c.dtype = kd;
-      c.op = ko;
-      c.avg_div = size_;
-      c.bytes = bytes;
-      for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
-      c.out[0] = wo.data_ptr();
-      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
-    } else {
-      const void* src;
-      at::Tensor stg;
-      if (is_flat(wi, bytes)) {
-        src = wi[0].data_ptr();
-      } else {  // K2 pack into one staging buffer
-        stg = at::empty({(int64_t)(bytes * size_)}, out.options().dtype(at::kByte));
-        std::vector<kern::CopyDesc> d;
-        for (int r = 0; r < size_; ++r) d.push_back({wi[r].data_ptr(), static_cast<char*>(stg.data_ptr()) + r * bytes, bytes});
-        multi_copy_or_memcpy(d, s);
-        src = stg.data_ptr();
-      }
-      PDCC_NCCL(ncclReduceScatter(src, wo.data_ptr(), out.numel(), nd, no, rc->get(), s));
-    }
+    enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, ds, s, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
   record(Coll::REDUCE_SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
@@ -903,7 +1325,6 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::Tensor>& outs,
                                                                 std::vector<at::Tensor>& ins, bool equal,
                                                                 std::chrono::milliseconds to) {
-  DeviceState& ds = dev_state(ins[0]);
   const auto t0 = std::chrono::steady_clock::now();
   size_t total = 0;
   for (auto& i : ins) total += i.nbytes();
@@ -912,31 +1333,33 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     record(Coll::ALLTOALL, "local", total, t0);
     return cpu_done(Coll::ALLTOALL, outs);
   }
+  DeviceState& ds = dev_state(ins[0]);
   const size_t chunk = ins[0].nbytes();
-  const Algo a = choose(Coll::ALLTOALL, equal ? chunk : SIZE_MAX, ds, ds.rccl_ok, ds.ipc_ok && equal);
+  const bool ipc_can = ds.ipc_ok && equal;
+  const Algo a0 = choose(Coll::ALLTOALL, equal ? chunk : SIZE_MAX, ds, ds.rccl_ok, ipc_can);
+  std::vector<at::Tensor> wi, wo;
+  for (auto& i : ins) wi.push_back(prep_in(i));
+  for (auto& o : outs) wo.push_back(prep_out(o));
+  const bool flat = equal && is_flat(wi, chunk) && is_flat(wo, chunk);
+  const Algo a = !equal ? a0 : decide(Coll::ALLTOALL, -1, flat ? kLayoutFlat : kLayoutList, chunk, ds, a0,
+                                      ds.rccl_ok, ipc_can, [&](const TuneKey& key, const std::vector<Algo>& cands) {
+    const int64_t n = sample_numel(wi[0].numel(), wi[0].element_size(), cfg_.autotune_sample, size_);
+    const std::vector<at::Tensor> si = sample_inputs(wi, n, flat);
+    std::vector<std::vector<at::Tensor>> sc;
+    for (size_t k = 0; k < cands.size(); ++k) sc.push_back(scratch_outputs(wo[0].options(), size_, n, flat));
+    const hipStream_t cs = current_stream(ds.device);
+    return autotune(
+        key, chunk, ds, cands, [&](size_t k) { enqueue_alltoall(cands[k], si, sc[k], true, ds, cs, to); },
+        [&](size_t r, size_t k) { return lists_equal(sc[r], sc[k]); });
+  });
   if (a == Algo::HOST) {
-    std::vector<at::Tensor> hi, ho;
-    std::vector<const void*> ip;
-    std::vector<void*> op;
-    std::vector<size_t> sb, rb;
-    for (auto& i : ins) {
-      hi.push_back(i.cpu().contiguous());
-      ip.push_back(hi.back().data_ptr());
-      sb.push_back(hi.back().nbytes());
-    }
-    for (auto& o : outs) {
-      ho.push_back(at::empty(o.sizes(), o.options().device(at::kCPU)));
-      op.push_back(ho.back().data_ptr());
-      rb.push_back(ho.back().nbytes());
-    }
-    shm().alltoall(ip, sb, op, rb, to);
-    for (size_t i = 0; i < outs.size(); ++i) outs[i].copy_(ho[i]);
+    enqueue_alltoall(Algo::HOST, wi, wo, equal, ds, current_stream(ds.device), to);
+    for (size_t i = 0; i < outs.size(); ++i)
+      if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
     record(Coll::ALLTOALL, "host", total, t0);
     return cpu_done(Coll::ALLTOALL, outs);
   }
-  std::vector<at::Tensor> wi, wo, keep;
-  for (auto& i : ins) wi.push_back(prep_in(i));
-  for (auto& o : outs) wo.push_back(prep_out(o));
+  std::vector<at::Tensor> keep;
   for (auto& x : wi) keep.push_back(x);
   for (auto& x : wo) keep.push_back(x);
   std::shared_ptr<IpcComm> icp;
@@ -944,33 +1367,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     ipc(ds);
     icp = ds.ipc;
   }
-  RcclComm* rc = (a == Algo::RCCL) ? &rccl(ds) : nullptr;
   auto work = gpu_run(Coll::ALLTOALL, ds, keep, outs, to, [&](hipStream_t s) {
-    if (a == Algo::IPC) {
-      kern::IpcCall c{};
-      c.coll = kern::IpcColl::ALLTOALL;
-      c.dtype = kern::DType::U8;
-      c.op = kern::RedOp::COPY;
-      c.bytes = chunk;
-      for (int r = 0; r < size_; ++r) {
-        c.in[r] = wi[r].data_ptr();
-        c.out[r] = wo[r].data_ptr();
-      }
-      ipc_chunked(*icp, c, icp->max_staging() / size_, s);
-    } else if (equal && is_flat(wi, chunk) && is_flat(wo, chunk)) {
-      PDCC_NCCL(ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc->get(), s));
-    } else {
-      PDCC_NCCL(ncclGroupStart());
-      for (int r = 0; r < size_; ++r) {
-        if (r == rank_) continue;
-        if (wi[r].nbytes()) PDCC_NCCL(ncclSend(wi[r].data_ptr(), wi[r].nbytes(), ncclUint8, r, rc->get(), s));
-        if (wo[r].nbytes()) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), wo[r].nbytes(), ncclUint8, r, rc->get(), s));
-      }
-      PDCC_NCCL(ncclGroupEnd());
-      if (wi[rank_].nbytes())
-        PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi[rank_].data_ptr(), wi[rank_].nbytes(),
-                                hipMemcpyDeviceToDevice, s));
-    }
+    enqueue_alltoall(a, wi, wo, equal, ds, s, to);
     for (size_t i = 0; i < outs.size(); ++i)
       if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
   }, icp);
@@ -979,45 +1377,70 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
 }
 
 // =================================================================== p2p + coalescing
-c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int peer, bool is_send,
-                                                           std::chrono::milliseconds to) {
-  DeviceState& ds = dev_state(t);
+// Host-staged point-to-point (ranks sharing a GPU, or PDCC_ALGO=host): the copy to
+// the host happens now, on the caller's stream; the transfer runs on the backend's
+// send/recv threads over the pair's shared-memory channel, so isend/irecv pairs
+// and rings never deadlock; the copy back to the GPU happens on the recv thread.
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::host_p2p(at::Tensor& t, int peer, bool is_send,
+                                                            std::chrono::milliseconds to) {
+  TORCH_CHECK(!capturing_on(t.device().index()), "pdcc: ", is_send ? "send" : "recv",
+              " runs on the host transport here, which cannot be captured into a graph");
   const auto t0 = std::chrono::steady_clock::now();
   const Coll cname = is_send ? Coll::SEND : Coll::RECV;
-  if (!ds.rccl_ok || cfg_.force_algo == Algo::HOST) {
-    TORCH_CHECK(!capturing_on(ds.device), "pdcc: ", is_send ? "send" : "recv",
-                " runs on the host transport here, which cannot be captured into a graph");
-    // shared-device setups: through the host transport, synchronously
-    if (is_send) {
-      at::Tensor h = t.cpu().contiguous();
-      shm().send(h.data_ptr(), h.nbytes(), peer, to);
-    } else {
-      at::Tensor h = at::empty(t.sizes(), t.options().device(at::kCPU));
-      shm().recv(h.data_ptr(), h.nbytes(), peer, to);
-      t.copy_(h);
-    }
-    record(cname, "host", t.nbytes(), t0);
-    return cpu_done(cname, {t});
+  auto work = c10::make_intrusive<WorkMI355X>(rank_, is_send ? c10d::OpType::SEND : c10d::OpType::RECV,
+                                              op_seq_.load(), std::vector<at::Tensor>{t});
+  const int pi = peer < rank_ ? 0 : 1;  // the peer's rank inside the pair channel
+  if (is_send) {
+    at::Tensor h = t.cpu().contiguous();
+    p2p_submit(true, Job{[this, h, peer, pi, to] { shm_pair(peer).send(h.data_ptr(), h.nbytes(), pi, to); }, work});
+  } else {
+    p2p_submit(false, Job{[this, t, peer, pi, to]() mutable {
+                            at::Tensor h = at::empty(t.sizes(), t.options().device(at::kCPU));
+                            shm_pair(peer).recv(h.data_ptr(), h.nbytes(), pi, to);
+                            c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+                            t.copy_(h);
+                            PDCC_HIP(hipStreamSynchronize(current_stream(t.device().index())));
+                          },
+                          work});
   }
-  RcclComm& rc = rccl(ds);
-  at::Tensor w = is_send ? prep_in(t) : prep_out(t);
-  auto op = [w, t, peer, is_send, comm = rc.get()](hipStream_t s) mutable {
-    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
-    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
-  };
+  if (coalescing_) coalesced_cpu_.push_back(work);
+  record(cname, "host", t.nbytes(), t0);
+  return work;
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int peer, bool is_send,
+                                                           std::chrono::milliseconds to) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const Coll cname = is_send ? Coll::SEND : Coll::RECV;
   if (coalescing_) {
-    coalesced_.push_back(op);
+    // batch_isend_irecv: one group call on the group's communicator (like ProcessGroupNCCL,
+    // every rank of the group takes part in the batch that first uses it)
+    DeviceState& ds = dev_state(t);
+    if (!ds.rccl_ok || cfg_.force_algo == Algo::HOST) return host_p2p(t, peer, is_send, to);
+    RcclComm& rc = rccl(ds);
+    at::Tensor w = is_send ? prep_in(t) : prep_out(t);
+    coalesced_.push_back([w, peer, is_send, comm = rc.get()](hipStream_t s) mutable {
+      if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
+      else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, peer, comm, s));
+    });
     coalesced_tensors_.push_back(t);
     coalesced_tensors_.push_back(w);
     coalesced_ds_ = &ds;
     record(cname, "rccl_coalesced", t.nbytes(), t0);
     return cpu_done(cname, {t});
   }
+  // single send/recv: only this pair of ranks takes part
+  DeviceState& ds = dev_local(t);
+  if (cfg_.force_algo == Algo::HOST || !pair_on_distinct_devices(ds, peer)) return host_p2p(t, peer, is_send, to);
+  RcclComm& rc = rccl_pair(ds, peer);
+  const int pi = peer < rank_ ? 0 : 1;
+  at::Tensor w = is_send ? prep_in(t) : prep_out(t);
   auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    op(s);
+    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, pi, rc.get(), s));
+    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, pi, rc.get(), s));
     if (!is_send && !w.is_same(t)) t.copy_(w);
   });
-  record(cname, "rccl", t.nbytes(), t0);
+  record(cname, "rccl_pair", t.nbytes(), t0);
   return work;
 }
 

@@ -11,6 +11,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <sstream>
 
@@ -320,6 +321,7 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
       group_name_(std::move(group_name)),
       cfg_(Config::from_env()),
       health_(std::make_shared<Health>()) {
+  members_key_ = make_members_key(global_ranks_, size);
   if (!cfg_.fault.empty()) {
     unsigned long long s = 0;
     char kind[32] = {0};
@@ -359,12 +361,49 @@ ProcessGroupMI355X::~ProcessGroupMI355X() {
   if (recv_thr_.joinable()) recv_thr_.join();
   for (auto& kv : devs_) {
     DeviceState& ds = *kv.second;
-    if (health_->poisoned.load() && ds.rccl) ds.rccl->abort();
+    if (!health_->poisoned.load()) continue;
+    if (ds.rccl) ds.rccl->abort();
+    for (auto& p : ds.pair_rccl) p.second->abort();
   }
 }
 
 std::chrono::milliseconds ProcessGroupMI355X::eff_timeout(std::chrono::milliseconds t) const {
   return t == c10d::kUnsetTimeout ? timeout_ : t;
+}
+
+// 2-rank shared-memory channel pair for point-to-point with `peer`: built by the
+// two ranks alone (lazily, on the send/recv worker threads), so send/recv never
+// wait for the other ranks of the group. One mutex per peer: the send and recv
+// threads may both ask for the same pair, and different pairs never block each other.
+host::ShmComm& ProcessGroupMI355X::shm_pair(int peer) {
+  std::shared_ptr<std::mutex> m;
+  {
+    std::lock_guard<std::mutex> lk(pair_mu_);
+    auto it = shm_pairs_.find(peer);
+    if (it != shm_pairs_.end()) return *it->second;
+    auto& pm = shm_pair_mu_[peer];
+    if (!pm) pm = std::make_shared<std::mutex>();
+    m = pm;
+  }
+  std::lock_guard<std::mutex> plk(*m);
+  {
+    std::lock_guard<std::mutex> lk(pair_mu_);
+    auto it = shm_pairs_.find(peer);
+    if (it != shm_pairs_.end()) return *it->second;
+  }
+  TORCH_CHECK(same_host_, "pdcc: the shared-memory host path needs every rank of the group on one host");
+  host::ShmConfig sc;
+  sc.slot_bytes = 4096;  // collectives never run on a pair channel
+  sc.spin_us = cfg_.shm_spin_us;
+  sc.chan_bytes = cfg_.shm_chan_bytes;
+  sc.timeout = timeout_;
+  const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
+  auto c = std::make_unique<host::ShmComm>(store_, "pdcc/shmp2p/" + std::to_string(lo) + ":" + std::to_string(hi),
+                                           rank_ == lo ? 0 : 1, 2, sc);
+  std::lock_guard<std::mutex> lk(pair_mu_);
+  host::ShmComm& ref = *c;
+  shm_pairs_[peer] = std::move(c);
+  return ref;
 }
 
 host::ShmComm& ProcessGroupMI355X::shm() {
@@ -432,6 +471,14 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
       throw std::runtime_error(o.str());
     }
   }
+}
+
+void ProcessGroupMI355X::record_setup(const std::string& key, std::chrono::steady_clock::time_point t0) {
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  OpStats& s = stats_[key];
+  s.calls++;
+  s.host_ms += ms;
 }
 
 void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0) {
@@ -507,10 +554,16 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
   health_->poison(why);
   {
     std::lock_guard<std::mutex> lk(init_mu_);
-    for (auto& kv : devs_)
-      if (kv.second->rccl) kv.second->rccl->abort();
+    for (auto& kv : devs_) {
+      DeviceState& ds = *kv.second;
+      if (ds.rccl) ds.rccl->abort();
+      for (auto& p : ds.pair_rccl) p.second->abort();
+      if (ds.ipc) ds.ipc->abort();  // kernels spinning in a cross-GPU barrier leave it
+    }
     if (shm_) shm_->abort();
   }
+  std::lock_guard<std::mutex> lk(pair_mu_);
+  for (auto& kv : shm_pairs_) kv.second->abort();
 }
 
 void ProcessGroupMI355X::set_algo(const std::string& a) {
@@ -579,13 +632,17 @@ void ProcessGroupMI355X::watchdog_loop() {
     std::lock_guard<std::mutex> lk(init_mu_);
     for (auto& kv : devs_) {
       DeviceState& ds = *kv.second;
-      if (ds.rccl) {
-        ncclResult_t r = ds.rccl->async_error();
+      std::vector<RcclComm*> comms;
+      if (ds.rccl) comms.push_back(ds.rccl.get());
+      for (auto& p : ds.pair_rccl) comms.push_back(p.second.get());
+      for (RcclComm* c : comms) {
+        ncclResult_t r = c->async_error();
         if (r != ncclSuccess && r != ncclInProgress) {
           const std::string m = std::string("RCCL async error: ") + ncclGetErrorString(r);
           fprintf(stderr, "[pdcc] rank %d: %s\n", rank_, m.c_str());
           health_->poison(m);
-          ds.rccl->abort();
+          c->abort();
+          if (ds.ipc) ds.ipc->abort();
         }
       }
       if (ds.ipc && ds.ipc->error_word() != 0 && !health_->poisoned.load()) {
@@ -939,8 +996,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::send(std::vector<at::Tensor>&
   at::Tensor c = t.contiguous();
   auto work = c10::make_intrusive<WorkMI355X>(rank_, c10d::OpType::SEND, op_seq_.load(), std::vector<at::Tensor>{t});
   auto to = timeout_;
-  host::ShmComm* sc = &shm();
-  p2p_submit(true, Job{[sc, c, dst, to] { sc->send(c.data_ptr(), c.nbytes(), dst, to); }, work});
+  const int pi = dst < rank_ ? 0 : 1;  // the peer's rank inside the pair channel
+  // the pair channel is built on the worker thread: a ring of first isends cannot deadlock
+  p2p_submit(true, Job{[this, c, dst, pi, to] { shm_pair(dst).send(c.data_ptr(), c.nbytes(), pi, to); }, work});
   if (coalescing_) coalesced_cpu_.push_back(work);
   return work;
 }
@@ -954,10 +1012,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::recv(std::vector<at::Tensor>&
   if (t.is_cuda()) return gpu_p2p(t, src, false, timeout_);
   auto work = c10::make_intrusive<WorkMI355X>(rank_, c10d::OpType::RECV, op_seq_.load(), std::vector<at::Tensor>{t});
   auto to = timeout_;
-  host::ShmComm* sc = &shm();
-  p2p_submit(false, Job{[sc, t, src, to]() mutable {
+  const int pi = src < rank_ ? 0 : 1;
+  p2p_submit(false, Job{[this, t, src, pi, to]() mutable {
                           at::Tensor c = t.is_contiguous() ? t : at::empty_like(t, at::MemoryFormat::Contiguous);
-                          sc->recv(c.data_ptr(), c.nbytes(), src, to);
+                          shm_pair(src).recv(c.data_ptr(), c.nbytes(), pi, to);
                           if (!c.is_same(t)) t.copy_(c);
                         },
                         work});

@@ -29,6 +29,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../device/ipc_comm.h"
@@ -142,11 +143,17 @@ class WorkMI355X : public c10d::Work {
 struct DeviceState {
   int device = -1;
   c10::hip::HIPStreamMasqueradingAsCUDA stream;  // comm stream for async collectives (PDCC_STREAM)
+  // group topology: filled by the first collective on this device (init_topology,
+  // collective over the group); point-to-point never needs it
+  bool topo = false;
+  std::vector<std::string> recs;        // "host|pci bus" of every rank (topology exchange)
   bool rccl_ok = false;                 // all ranks on distinct devices
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
   bool shared_device = false;           // several ranks share one GPU (test setups)
-  std::unique_ptr<RcclComm> rccl;       // lazy
+  std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
   std::shared_ptr<IpcComm> ipc;         // lazy
+  std::map<int, std::shared_ptr<RcclComm>> pair_rccl;  // 2-rank communicators for send/recv, by peer
+  std::map<int, bool> pair_distinct;                   // peer on another device (RCCL-capable pair)?
   std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
   std::shared_ptr<StreamSync> sync = std::make_shared<StreamSync>();
   explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
@@ -238,9 +245,18 @@ class ProcessGroupMI355X : public c10d::Backend {
 
   std::chrono::milliseconds eff_timeout(std::chrono::milliseconds t) const;
   host::ShmComm& shm();
+  // 2-rank host channel to `peer` (lazy, only the two ranks take part)
+  host::ShmComm& shm_pair(int peer);
+  // device state without the group-wide topology exchange (non-collective)
+  DeviceState& dev_local(const at::Tensor& t);
+  // device state + topology (collective over the group on first use)
   DeviceState& dev_state(const at::Tensor& t);
+  void init_topology(DeviceState& ds);
   RcclComm& rccl(DeviceState& ds);
+  RcclComm& rccl_pair(DeviceState& ds, int peer);
+  bool pair_on_distinct_devices(DeviceState& ds, int peer);
   IpcComm& ipc(DeviceState& ds);
+  RcclOpts rccl_opts() const;
   // PDCC_IPC_SELFTEST: run the IPC protocol once on known data; false = IPC off for this group
   bool ipc_selftest(DeviceState& ds);
   Algo choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can);
@@ -248,6 +264,9 @@ class ProcessGroupMI355X : public c10d::Backend {
   void debug_check(Coll c, const std::vector<at::Tensor>& ts, int root);
   void maybe_inject_fault();
   void record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0);
+  // one-time setup cost (communicator creation ...) as a stats() row
+  void record_setup(const std::string& key, std::chrono::steady_clock::time_point t0);
+  static std::string make_members_key(const std::vector<int64_t>& global_ranks, int size);
 
   // GPU plumbing: run `fn(stream)` on the comm stream after the current stream
   c10::intrusive_ptr<c10d::Work> gpu_run(Coll c, DeviceState& ds, const std::vector<at::Tensor>& keep_alive,
@@ -283,6 +302,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> gpu_alltoall(std::vector<at::Tensor>& outs, std::vector<at::Tensor>& ins,
                                               bool equal_split, std::chrono::milliseconds to);
   c10::intrusive_ptr<c10d::Work> gpu_p2p(at::Tensor& t, int peer, bool is_send, std::chrono::milliseconds to);
+  c10::intrusive_ptr<c10d::Work> host_p2p(at::Tensor& t, int peer, bool is_send, std::chrono::milliseconds to);
 
   c10::intrusive_ptr<c10d::Store> store_;
   std::chrono::milliseconds timeout_;
@@ -292,8 +312,12 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::shared_ptr<Health> health_;
   bool same_host_ = true;
 
+  std::string members_key_;  // sorted global ranks: identifies groups with the same member set
   std::mutex init_mu_;
   std::unique_ptr<host::ShmComm> shm_;
+  std::mutex pair_mu_;
+  std::map<int, std::shared_ptr<std::mutex>> shm_pair_mu_;
+  std::map<int, std::unique_ptr<host::ShmComm>> shm_pairs_;
   std::map<int, std::unique_ptr<DeviceState>> devs_;
 
   std::atomic<uint64_t> op_seq_{0};
@@ -333,13 +357,15 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::vector<FrRecord> flight_recorder();
   std::string flight_recorder_dump(size_t last = 16);
 
-  // autotuner decisions so far: one row per (collective, power-of-two size bucket)
+  // autotuner decisions so far: one row per (collective, dtype, op, power-of-two size bucket)
   struct TuneRecord {
-    std::string coll;
-    uint64_t lo, hi;  // bucket [lo, hi) in bytes
+    std::string coll, dtype, op;
+    uint64_t lo, hi;  // bucket [lo, hi) in bytes (per-rank payload, see tune_bytes in gpu_ops.cpp)
+    std::string ref;  // reference engine: rccl, or host where RCCL is unavailable
     double rccl_us, ipc_us;
-    bool valid;       // IPC result matched RCCL's on every rank
+    bool valid;       // IPC result matched the reference engine's on every rank
     std::string algo;
+    int iters;        // timed runs per engine (median taken)
   };
   std::vector<TuneRecord> autotune_table();
 
@@ -350,23 +376,45 @@ class ProcessGroupMI355X : public c10d::Backend {
 
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
+    Algo ref = Algo::RCCL;
     double rccl_us = 0, ipc_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
+    int iters = 0;
   };
-  std::map<std::pair<int, int>, TuneEntry> tune_;  // (coll, floor(log2 bytes)) -> decision
+  // (coll, dtype or -1, reduce op or -1 (copies: list layout), floor(log2 bytes)) -> decision
+  using TuneKey = std::tuple<int, int, int, int>;
+  std::map<TuneKey, TuneEntry> tune_;
   std::mutex tune_mu_;
   // engines worth timing for this call (reference engine first); empty = no tuning
   std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const;
-  Algo tuned(Coll c, size_t bytes);
-  // run every candidate once on its own scratch copy via `run(k)`, check `same(0, k)` against
-  // the reference, time `iters` more runs each, agree across ranks (host transport), remember
-  // and return the winner
-  Algo autotune(Coll c, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
+  Algo tuned(const TuneKey& k);
+  // engine for one call: the static choice `a0`, or the tuned one for this key (tuning now,
+  // through `tune(cands)`, when the key has no decision yet)
+  Algo decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can, bool ipc_can,
+              const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune);
+  // run every candidate once via `run(k)` (on scratch buffers), check `same(0, k)` against the
+  // reference, then time interleaved runs of each (median), agree across ranks (host transport),
+  // remember and return the winner
+  Algo autotune(const TuneKey& key, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
                 const std::function<void(size_t)>& run, const std::function<bool(size_t, size_t)>& same);
+
+  // one engine's enqueue of each collective on stream `s` (HOST: synchronous)
   void enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko, ncclDataType_t nd,
-                         ncclRedOp_t no, c10d::ReduceOp::RedOpType op, int root, bool rooted, DeviceState& ds,
-                         hipStream_t s, std::chrono::milliseconds to);
+                         ncclRedOp_t no, bool nok, c10d::ReduceOp::RedOpType op, int root, bool rooted,
+                         DeviceState& ds, hipStream_t s, std::chrono::milliseconds to);
+  void enqueue_broadcast(Algo a, const at::Tensor& w, int root, DeviceState& ds, hipStream_t s,
+                         std::chrono::milliseconds to);
+  void enqueue_allgather(Algo a, const at::Tensor& wi, const std::vector<at::Tensor>& wo, int root, bool rooted,
+                         DeviceState& ds, hipStream_t s, std::chrono::milliseconds to);
+  void enqueue_scatter(Algo a, const std::vector<at::Tensor>& wi, const at::Tensor& wo, int root, DeviceState& ds,
+                       hipStream_t s, std::chrono::milliseconds to);
+  void enqueue_reduce_scatter(Algo a, const std::vector<at::Tensor>& wi, const at::Tensor& wo, kern::DType kd,
+                              kern::RedOp ko, ncclDataType_t nd, ncclRedOp_t no, bool nok,
+                              c10d::ReduceOp::RedOpType op, DeviceState& ds, hipStream_t s,
+                              std::chrono::milliseconds to);
+  void enqueue_alltoall(Algo a, const std::vector<at::Tensor>& wi, const std::vector<at::Tensor>& wo, bool equal,
+                        DeviceState& ds, hipStream_t s, std::chrono::milliseconds to);
 
   std::mutex stats_mu_;
   std::map<std::string, OpStats> stats_;

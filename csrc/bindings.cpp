@@ -117,12 +117,16 @@ PYBIND11_MODULE(_C, m) {
              for (const auto& r : pg.autotune_table()) {
                py::dict d;
                d["coll"] = r.coll;
+               d["dtype"] = r.dtype;
+               d["op"] = r.op;
                d["lo"] = r.lo;
                d["hi"] = r.hi;
+               d["ref"] = r.ref;
                d["ref_us"] = r.rccl_us;
                d["ipc_us"] = r.ipc_us;
                d["ipc_valid"] = r.valid;
                d["algo"] = r.algo;
+               d["iters"] = r.iters;
                l.append(d);
              }
              return l;
@@ -157,6 +161,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
         "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);
+  m.def("forwarded_rccl_env", &pdcc::forward_rccl_env,
+        "NCCL_* variables set from PDCC_RCCL_* before the first communicator (once per process)");
   m.attr("MAX_RANKS_IPC") = pdcc::kern::kMaxRanks;
   m.attr("TILE_BYTES") = pdcc::kern::kTileBytes;
 }

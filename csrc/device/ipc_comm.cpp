@@ -269,5 +269,10 @@ uint32_t IpcComm::error_word() const { return err_host_ ? __atomic_load_n(err_ho
 void IpcComm::clear_error() {
   if (err_host_) __atomic_store_n(err_host_, 0u, __ATOMIC_RELEASE);
 }
+void IpcComm::abort() {
+  if (!err_host_) return;
+  uint32_t expect = 0;
+  __atomic_compare_exchange_n(err_host_, &expect, kAbortWord, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+}
 
 }  // namespace pdcc

@@ -50,6 +50,10 @@ class IpcComm {
   // Error word written by a kernel whose spin timed out (0 = healthy).
   uint32_t error_word() const;
   void clear_error();
+  // Host-side abort (watchdog / abort_group): sets the error word to kAbortWord;
+  // kernels spinning in a cross-GPU barrier see it within ~256 polls and leave.
+  static constexpr uint32_t kAbortWord = 0x200u;
+  void abort();
   bool shared_device() const { return shared_device_; }
   int world() const { return world_; }
   uint64_t calls() const { return seq_; }

@@ -387,7 +387,7 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
     }
     const uint32_t* mine = v.flags[v.rank] + b * kern::kMaxRanks;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
+    for (uint32_t it = 1;; ++it) {
       bool me_ok = true;
       if (lane < v.world)
         me_ok = reached(__hip_atomic_load(mine + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), value);
@@ -395,6 +395,12 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
       if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
         if (lane == 0)
           __hip_atomic_store(v.err, 0x100u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = false;
+        break;
+      }
+      // every 256 polls: has the host aborted the group (IpcComm::abort), or did
+      // another block already time out? Either way stop waiting, so the grid drains.
+      if ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
         ok = false;
         break;
       }

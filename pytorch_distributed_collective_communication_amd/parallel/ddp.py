@@ -14,13 +14,19 @@ contract, MI355X-first:
   gradient is produced (``register_post_accumulate_grad_hook``), so
   communication overlaps the rest of the backward pass on the backend's
   high-priority comm stream;
-* :meth:`finish` waits, averages (one fused scale) and unpacks.
+* :meth:`finish` waits, averages (one fused scale) and unpacks;
+* gradient accumulation: backward passes inside ``with bucketer.no_sync():``
+  only accumulate into ``.grad``; the first backward after it launches the
+  reduction of the accumulated gradients. A second backward before
+  :meth:`finish` (outside ``no_sync``) raises instead of silently dropping a
+  micro-batch.
 
 ``broadcast_parameters`` and ``scatter_batch`` cover the other two uses.
 torch's own ``DistributedDataParallel`` also runs unchanged on this backend.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Iterable, List
 
 import torch
@@ -82,7 +88,18 @@ class GradBucketer:
         if cur:
             self._add_bucket(cur)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
+        self._sync = True
         self._reset()
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes in this context accumulate gradients locally (no communication)."""
+        prev = self._sync
+        self._sync = False
+        try:
+            yield
+        finally:
+            self._sync = prev
 
     def _add_bucket(self, ps):
         b = _Bucket(ps, ps[0].dtype, ps[0].device)
@@ -97,8 +114,14 @@ class GradBucketer:
             b.work = None
 
     def _on_grad(self, p: torch.nn.Parameter):
+        if not self._sync:
+            return
         bi, i = self._where[id(p)]
         b = self.buckets[bi]
+        if b.pending <= 0:
+            raise RuntimeError(
+                "GradBucketer: a gradient arrived for a bucket that is already being reduced -- two backward "
+                "passes without finish() in between; wrap the accumulation steps in `with bucketer.no_sync():`")
         off = b.offsets[i]
         b.flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
         b.pending -= 1

@@ -33,6 +33,8 @@ for s in "$@"; do
     pmc) PDCC_PMC_ONLY=1 step pmc 600 bash scripts/profile.sh ;;
     trace) PDCC_TRACE_ONLY=1 step trace 900 bash scripts/profile.sh ;;
     k2sweep) step k2sweep 300 python scripts/k2_sweep.py ;;
+    bench2self) PDCC_BENCH_SMALL=1 step bench2self 600 python bench.py --gpus 2 --steps 3 --warmup 1 --bytes 67108864 ;;
+    churn) step churn 300 python scripts/group_churn.py ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;

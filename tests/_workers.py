@@ -462,6 +462,97 @@ def autotune_probe(rank, size, device="cuda"):
     return {"ok": ok, "table": be.autotune_table()}
 
 
+def autotune_all_colls(rank, size, device="cuda", n=1 << 16):
+    """Every tunable collective once at a tunable size (256 KiB of fp32): each call
+    must be right, and the table must get one row per (collective, dtype, op,
+    layout) -- identical on every rank. Then the ADVICE r1 case: a float SUM
+    bucket decided first, an int32 BAND of the same size afterwards (no RCCL op
+    exists for BAND: the key must not inherit the float decision)."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    ok = {}
+    base = torch.arange(n, device=d, dtype=torch.float32) % 97
+    t = base + rank
+    dist.all_reduce(t)
+    ok["all_reduce"] = bool(torch.equal(t, base * size + size * (size - 1) / 2))
+    t = base + rank
+    dist.reduce(t, dst=size - 1)
+    ok["reduce"] = rank != size - 1 or bool(torch.equal(t, base * size + size * (size - 1) / 2))
+    t = base.clone() if rank == 0 else torch.zeros_like(base)
+    dist.broadcast(t, src=0)
+    ok["broadcast"] = bool(torch.equal(t, base))
+    out = torch.empty(n * size, device=d)
+    dist.all_gather_into_tensor(out, base + rank)
+    ok["all_gather_flat"] = all(bool(torch.equal(out[r * n:(r + 1) * n], base + r)) for r in range(size))
+    lst = [torch.empty(n, device=d) for _ in range(size)]
+    dist.all_gather(lst, base + rank)
+    ok["all_gather_list"] = all(bool(torch.equal(lst[r], base + r)) for r in range(size))
+    glist = [torch.empty(n, device=d) for _ in range(size)] if rank == 0 else None
+    dist.gather(base + rank, gather_list=glist, dst=0)
+    ok["gather"] = rank != 0 or all(bool(torch.equal(glist[r], base + r)) for r in range(size))
+    slist = [base + 1000 * r for r in range(size)] if rank == 0 else None
+    so = torch.empty(n, device=d)
+    dist.scatter(so, scatter_list=slist, src=0)
+    ok["scatter"] = bool(torch.equal(so, base + 1000 * rank))
+    inp = torch.cat([base + r for r in range(size)]) * (rank + 1)
+    rs = torch.empty(n, device=d)
+    dist.reduce_scatter_tensor(rs, inp)
+    ok["reduce_scatter"] = bool(torch.equal(rs, (base + rank) * (size * (size + 1) / 2)))
+    a2a_in = torch.cat([base + 100 * rank + q for q in range(size)])
+    a2a_out = torch.empty_like(a2a_in)
+    dist.all_to_all_single(a2a_out, a2a_in)
+    ok["all_to_all"] = all(bool(torch.equal(a2a_out[q * n:(q + 1) * n], base + 100 * q + rank)) for q in range(size))
+    # ADVICE r1: same size bucket, different dtype/op
+    m = 25_600  # 100 KiB of fp32 / int32
+    f = torch.full((m,), float(rank + 1), device=d)
+    dist.all_reduce(f)
+    ok["float_sum_100k"] = bool(torch.all(f == size * (size + 1) / 2))
+    bits = torch.full((m,), (1 << rank) | 0x100, device=d, dtype=torch.int32)
+    dist.all_reduce(bits, op=dist.ReduceOp.BAND)
+    ok["int_band_100k"] = bool(torch.all(bits == 0x100))
+    bits = torch.full((m,), 1 << rank, device=d, dtype=torch.int32)
+    dist.all_reduce(bits, op=dist.ReduceOp.BOR)
+    ok["int_bor_100k"] = bool(torch.all(bits == (1 << size) - 1))
+    return {"ok": ok, "table": be.autotune_table()}
+
+
+def group_churn(rank, size, device="cuda", groups=6):
+    """The reference's pattern: a fresh new_group(range(size)) per demo
+    (main.py:11,21,31,46,63,75), one collective in each. Returns per-group wall
+    time of (new_group + first all_reduce) and how each group got its RCCL
+    communicator (stats rows rccl_comm/<init|split|share>)."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    x = torch.ones(1024, device=d)
+    t0 = time.perf_counter()
+    dist.all_reduce(x)
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    ok = [bool(torch.all(x == size))]
+    out = []
+    for _ in range(groups):
+        t0 = time.perf_counter()
+        g = dist.new_group(list(range(size)))
+        y = torch.ones(1024, device=d)
+        dist.all_reduce(y, group=g)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        ok.append(bool(torch.all(y == size)))
+        st = be.native_backend(g, "cuda").stats()
+        how = sorted(k.split("/", 1)[1] for k in st if k.startswith("rccl_comm/"))
+        setup_ms = sum(v[2] for k, v in st.items() if k.startswith("rccl_comm/"))
+        out.append({"wall_ms": dt * 1e3, "how": how, "comm_ms": setup_ms})
+    return {"ok": ok, "first_ms": first * 1e3, "groups": out}
+
+
 def graph_capture(rank, size, device="cuda", replays=5):
     """Collectives captured into a hipGraph (parallel.graphs.capture) and replayed
     with new inputs each time, with an eager collective between two replays: the
@@ -554,3 +645,108 @@ def gpu_fault_victim(rank, size, q, group_timeout_s=4):
 
     res = init_process(rank, size, body, bind_device=True, timeout_s=group_timeout_s)
     q.put((rank, res))
+
+
+def p2p_subset(rank, size, device="cpu", n=300_000):
+    """Point-to-point between two ranks of a larger group, issued before any
+    collective: ranks 0 and 1 exchange (both directions, larger than a channel),
+    the others do nothing until a later barrier. Then a ring of FIRST isends on
+    a fresh group (each pair channel is built by the two ranks alone)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ok = {}
+    if rank in (0, 1):
+        peer = 1 - rank
+        x = torch.full((n,), float(rank + 1), device=d)
+        y = torch.empty(n, device=d)
+        if rank == 0:
+            dist.send(x, peer)
+            dist.recv(y, peer)
+        else:
+            dist.recv(y, peer)
+            dist.send(x, peer)
+        ok["pair"] = bool(torch.all(y == peer + 1))
+    dist.barrier()
+    g = dist.new_group(list(range(size)))
+    nxt, prv = (rank + 1) % size, (rank - 1) % size
+    x = torch.full((n,), float(10 + rank), device=d)
+    y = torch.empty(n, device=d)
+    s = dist.isend(x, nxt, group=g)
+    r = dist.irecv(y, prv, group=g)
+    s.wait()
+    r.wait()
+    ok["ring_first_isend"] = bool(torch.all(y == 10 + prv))
+    return ok
+
+
+def dp_accum(rank, size, device="cpu", micro=2):
+    """Gradient accumulation with GradBucketer.no_sync(): `micro` micro-batches per
+    rank, one reduction per step; returns (params after one SGD step, whether a
+    second backward without no_sync() raised)."""
+    import torch
+
+    from pytorch_distributed_collective_communication_amd.models import MLP, synthetic_batch
+    from pytorch_distributed_collective_communication_amd.parallel import ddp
+
+    d = _dev(device)
+    torch.manual_seed(100 + rank)
+    model = MLP().to(d)
+    ddp.broadcast_parameters(model, src=0)
+    x, y = synthetic_batch(64, device=d)
+    shard = 64 // size
+    xs, ys = x[rank * shard:(rank + 1) * shard], y[rank * shard:(rank + 1) * shard]
+    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    buck = ddp.GradBucketer(model, bucket_bytes=2048)
+    opt.zero_grad(set_to_none=False)
+    mb = shard // micro
+    for k in range(micro):
+        loss = torch.nn.functional.mse_loss(model(xs[k * mb:(k + 1) * mb]), ys[k * mb:(k + 1) * mb]) / micro
+        if k < micro - 1:
+            with buck.no_sync():
+                loss.backward()
+        else:
+            loss.backward()
+    buck.finish()
+    opt.step()
+    params = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()]).tolist()
+    raised = False
+    try:
+        for _ in range(2):
+            torch.nn.functional.mse_loss(model(xs), ys).backward()
+    except RuntimeError as e:
+        raised = "no_sync" in str(e)
+    return params, raised
+
+
+def engine_crosscheck(rank, size, device="cuda"):
+    """The same random inputs through RCCL and through the IPC kernels (forced per
+    call with set_algo, identically on every rank): results must agree (SUM
+    within summation-order rounding, MAX and the copy collectives exactly)."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    gen = torch.Generator(device=d).manual_seed(1000 + rank)
+    ok = {}
+    for n in (1000, 1 << 20, 3_000_017):
+        x = torch.randn(n, generator=gen, device=d)
+        res = {}
+        for algo in ("rccl", "ipc"):
+            b.set_algo(algo)
+            y = x.clone()
+            dist.all_reduce(y)
+            m = x.clone()
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+            lst = [torch.empty(n, device=d) for _ in range(size)]
+            dist.all_gather(lst, x)
+            res[algo] = (y, m, torch.cat(lst))
+        b.set_algo("auto")
+        ok[f"sum_{n}"] = bool(torch.allclose(res["rccl"][0], res["ipc"][0], rtol=1e-5, atol=1e-5 * size))
+        ok[f"max_{n}"] = bool(torch.equal(res["rccl"][1], res["ipc"][1]))
+        ok[f"all_gather_{n}"] = bool(torch.equal(res["rccl"][2], res["ipc"][2]))
+    return ok

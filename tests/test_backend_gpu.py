@@ -81,6 +81,12 @@ def test_shared_gpu_host_fallback():
         assert got == W.expected_golden(r, 2), (r, got)
 
 
+def test_shared_gpu_p2p_pairs_before_any_collective():
+    # send/recv between two ranks of a 3-rank group must not wait for the third
+    for ok in _gpu_launch(W.p2p_subset, 3, args=("cuda", 50_000)):
+        assert all(ok.values()), ok
+
+
 def test_shared_gpu_p2p_host_staged():
     for ok in _gpu_launch(W.p2p, 2, args=("cuda", 1000)):
         assert all(ok.values()), ok
@@ -133,7 +139,37 @@ def test_autotuner_shared_gpu():
     assert los == [64 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20], res[0]["table"]
     for e in res[0]["table"]:
         assert e["coll"] == "allreduce" and e["ipc_valid"], e
-        assert e["algo"] in ("ipc", "host")
+        assert e["algo"] in ("ipc", "host") and e["ref"] == "host"
+        assert e["dtype"] in ("Float", "BFloat16") and e["op"] == "SUM", e
+        assert e["iters"] >= 3
+
+
+def test_autotuner_every_collective_shared_gpu():
+    # every tunable collective gets its own measured decision (verdict r1 #4), keyed by
+    # dtype and op too (an int BAND must not inherit a float SUM decision)
+    res = _gpu_launch(W.autotune_all_colls, 2)
+    for r in res:
+        assert all(r["ok"].values()), r["ok"]
+    assert res[0]["table"] == res[1]["table"]
+    rows = {(e["coll"], e["dtype"], e["op"]) for e in res[0]["table"]}
+    for want in [("allreduce", "Float", "SUM"), ("reduce", "Float", "SUM"), ("broadcast", "-", "-"),
+                 ("allgather", "-", "flat"), ("allgather", "-", "list"), ("gather", "-", "-"),
+                 ("scatter", "-", "-"), ("reduce_scatter", "Float", "SUM"), ("alltoall", "-", "flat"),
+                 ("allreduce", "Int", "BAND"), ("allreduce", "Int", "BOR")]:
+        assert want in rows, (want, sorted(rows))
+    for e in res[0]["table"]:
+        assert e["ipc_valid"] and e["algo"] in ("ipc", "host"), e
+
+
+@pytest.mark.parametrize("mode", ["split", "share"])
+def test_group_churn_reuses_the_communicator(mode):
+    # main.py builds new_group(range(size)) in every demo: with PDCC_WORLD1_LOCAL=0 every
+    # group runs RCCL; after the first, groups derive their communicator from it
+    env = {"PDCC_WORLD1_LOCAL": "0", "PDCC_RCCL_GROUP_COMM": mode}
+    res = _gpu_launch(W.group_churn, 1, env=env)[0]
+    assert all(res["ok"]), res
+    for g in res["groups"]:
+        assert g["how"] == [mode], res
 
 
 @pytest.mark.parametrize("world,env", [

@@ -103,3 +103,10 @@ def test_peer_death_is_detected_quickly():
     assert "exited" in msg or "aborted" in msg, msg
     assert elapsed < 20, elapsed
     assert ps[1].exitcode == 13
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_p2p_between_two_ranks_of_a_larger_group(world):
+    # send/recv must not need the other ranks of the group (pair channels)
+    for ok in launch(W.p2p_subset, world, args=("cpu",), timeout_s=60, join_timeout_s=120):
+        assert all(ok.values()), ok

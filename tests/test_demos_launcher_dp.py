@@ -65,3 +65,13 @@ def test_data_parallel_matches_single_process(mode):
     for p in res:
         torch.testing.assert_close(p, res[0], rtol=0, atol=0)
         torch.testing.assert_close(p, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_gradient_accumulation_no_sync():
+    # two micro-batches per step (first under no_sync) == one full-batch step;
+    # a second backward without no_sync() must raise instead of dropping a micro-batch
+    res = launch(W.dp_accum, 2)
+    ref = W.dp_reference(steps=1)
+    for params, raised in res:
+        torch.testing.assert_close(torch.tensor(params), ref, rtol=1e-5, atol=1e-6)
+        assert raised
