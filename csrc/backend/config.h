@@ -52,9 +52,12 @@ struct Config {
   int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
   int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
   // Groups whose member set equals a live communicator's (new_group(range(size)) in every demo
-  // of the reference): split = ncclCommSplit from it (cheap), share = use the same communicator,
-  // init = always a fresh ncclCommInitRank.
-  int group_comm = 0;                      // PDCC_RCCL_GROUP_COMM=split|share|init (0|1|2)
+  // of the reference): share = use that communicator (RCCL runs the ops of one communicator in
+  // issue order on every stream, which is the order every rank issues them in), split =
+  // ncclCommSplit from it, init = always a fresh ncclCommInitRank. Measured on MI355X
+  // (profiles/group_churn.jsonl, 1-rank communicators): init 41-44 ms, split 40-44 ms,
+  // share 0.1 ms per group.
+  int group_comm = 1;                      // PDCC_RCCL_GROUP_COMM=split|share|init (0|1|2)
   bool rccl_split_share = true;            // PDCC_RCCL_SPLIT_SHARE: split children share parent resources
   // all_gather into a list of separate tensors on RCCL: p2p = grouped ncclSend/Recv straight
   // into the list (zero copy), staged = ncclAllGather into a staging buffer + K2 unpack

@@ -252,6 +252,16 @@ DeviceState& ProcessGroupMI355X::dev_local(const at::Tensor& t) {
   auto ds = std::make_unique<DeviceState>(
       c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
   ds->device = d;
+  // this rank's device record, for point-to-point peers (non-blocking: set only; a
+  // peer reads it after posting its own, so a ring of first ops cannot wait in a cycle)
+  store_->set("pdcc/devrec/" + std::to_string(rank_), [&] {
+    char bus[64] = {0};
+    PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
+    char host[256] = {0};
+    gethostname(host, sizeof(host) - 1);
+    const std::string rec = std::string(host) + "|" + bus;
+    return std::vector<uint8_t>(rec.begin(), rec.end());
+  }());
   DeviceState& ref = *ds;
   devs_[d] = std::move(ds);
   return ref;
@@ -385,27 +395,21 @@ RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
   return *ds.rccl;
 }
 
-// 2-rank communicator for send/recv with `peer`: only the two ranks take part
-// (ProcessGroupNCCL keeps one per pair the same way), so point-to-point between
-// two ranks of a larger group never waits for the others.
-RcclComm& ProcessGroupMI355X::rccl_pair(DeviceState& ds, int peer) {
-  {
-    std::lock_guard<std::mutex> lk(init_mu_);
-    auto it = ds.pair_rccl.find(peer);
-    if (it != ds.pair_rccl.end()) return *it->second;
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
-  auto c = std::make_shared<RcclComm>(store_, "pdcc/p2p/" + std::to_string(lo) + ":" + std::to_string(hi),
-                                      rank_ == lo ? 0 : 1, 2, ds.device, RcclOpts());
-  record_setup("rccl_comm/pair", t0);
+// The send/recv channel to `peer` (created on first use; its communicator is
+// built by the channel's own thread, see PairChan).
+std::shared_ptr<PairChan> ProcessGroupMI355X::pair_chan(DeviceState& ds, int peer) {
   std::lock_guard<std::mutex> lk(init_mu_);
-  ds.pair_rccl[peer] = c;
-  return *c;
+  auto it = ds.pairs.find(peer);
+  if (it != ds.pairs.end()) return it->second;
+  auto pc = std::make_shared<PairChan>(
+      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/false, (c10::DeviceIndex)ds.device));
+  ds.pairs[peer] = pc;
+  return pc;
 }
 
 // Are this rank and `peer` on different GPUs of one host? From the group topology when a
-// collective already exchanged it, else through a pairwise store exchange.
+// collective already exchanged it, else from the peer's device record (posted by its
+// first GPU op in this group, before it waits on anybody).
 bool ProcessGroupMI355X::pair_on_distinct_devices(DeviceState& ds, int peer) {
   {
     std::lock_guard<std::mutex> lk(init_mu_);
@@ -413,18 +417,10 @@ bool ProcessGroupMI355X::pair_on_distinct_devices(DeviceState& ds, int peer) {
     auto it = ds.pair_distinct.find(peer);
     if (it != ds.pair_distinct.end()) return it->second;
   }
-  char bus[64] = {0};
-  PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, ds.device));
-  char host[256] = {0};
-  gethostname(host, sizeof(host) - 1);
-  const std::string rec = std::string(host) + "|" + bus;
-  const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
-  const std::string key = "pdcc/p2pdev/" + std::to_string(lo) + ":" + std::to_string(hi) + "/";
-  store_->set(key + std::to_string(rank_), std::vector<uint8_t>(rec.begin(), rec.end()));
-  const auto v = store_->get(key + std::to_string(peer));
-  const std::string other(v.begin(), v.end());
-  const bool same_host = other.substr(0, other.find('|')) == std::string(host);
-  const bool distinct = same_host && other != rec;
+  const auto mine = store_->get("pdcc/devrec/" + std::to_string(rank_));
+  const auto theirs = store_->get("pdcc/devrec/" + std::to_string(peer));
+  const std::string a(mine.begin(), mine.end()), b(theirs.begin(), theirs.end());
+  const bool distinct = a.substr(0, a.find('|')) == b.substr(0, b.find('|')) && a != b;
   std::lock_guard<std::mutex> lk(init_mu_);
   ds.pair_distinct[peer] = distinct;
   return distinct;
@@ -573,15 +569,17 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
                                                            std::vector<at::Tensor> outputs,
                                                            std::chrono::milliseconds timeout,
                                                            const std::function<void(hipStream_t)>& fn,
-                                                           std::shared_ptr<IpcComm> ipcp) {
+                                                           std::shared_ptr<IpcComm> ipcp,
+                                                           const c10::hip::HIPStreamMasqueradingAsCUDA* stream) {
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
   // synchronous collectives (and PDCC_STREAM=current) run on the caller's stream: no
   // cross-stream event hand-off, which costs far more than the launch on this runtime
-  // (and graph capture always: the capturing stream is the only one the graph sees)
+  // (and graph capture always: the capturing stream is the only one the graph sees);
+  // point-to-point runs on its pair's own stream (`stream`)
   const bool cap = capturing(cur.stream());
-  const bool on_current = cap || cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_);
-  const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : ds.stream;
+  const bool on_current = cap || (!stream && (cfg_.stream_mode == 3 || (cfg_.stream_mode != 2 && !op_async_)));
+  const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : (stream ? *stream : ds.stream);
   StreamSync& sy = *ds.sync;
   bool use_sig = false;
   if (comm != cur) {
@@ -1432,16 +1430,104 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
   // single send/recv: only this pair of ranks takes part
   DeviceState& ds = dev_local(t);
   if (cfg_.force_algo == Algo::HOST || !pair_on_distinct_devices(ds, peer)) return host_p2p(t, peer, is_send, to);
-  RcclComm& rc = rccl_pair(ds, peer);
-  const int pi = peer < rank_ ? 0 : 1;
+  auto pc = pair_chan(ds, peer);
+  const int pi = peer < rank_ ? 0 : 1;  // the peer's rank in the pair communicator
   at::Tensor w = is_send ? prep_in(t) : prep_out(t);
+  {
+    std::unique_lock<std::mutex> lk(pc->mu);
+    if (!pc->error.empty()) throw std::runtime_error("pdcc: point-to-point channel to rank " + std::to_string(peer) +
+                                                     " failed: " + pc->error);
+    if (!(pc->ready && pc->q.empty())) {
+      // the channel's communicator is still being built: queue behind it, in order
+      TORCH_CHECK(!capturing_on(ds.device), "pdcc: the first send/recv between two ranks cannot be captured into a "
+                  "graph (it builds their communicator): run one exchange before capturing");
+      c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
+      auto gate = std::make_shared<Gate>();
+      PDCC_HIP(hipEventCreateWithFlags(&gate->ev, hipEventDisableTiming));
+      hipEvent_t after = nullptr;
+      PDCC_HIP(hipEventCreateWithFlags(&after, hipEventDisableTiming));
+      PDCC_HIP(hipEventRecord(after, current_stream(ds.device)));
+      pc->q.push_back({is_send, t, w, after, gate});
+      auto work = c10::make_intrusive<WorkMI355X>(
+          rank_, is_send ? c10d::OpType::SEND : c10d::OpType::RECV, op_seq_.load(), std::vector<at::Tensor>{t},
+          c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), gate->ev, pc->stream, health_, cfg_.blocking_wait,
+          to, nullptr, nullptr);
+      work->set_gate(gate);
+      if (!pc->started) {
+        pc->started = true;
+        // self-contained (copies only): the thread may outlive a group destroyed meanwhile
+        const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
+        std::thread([pc, store = store_, key = "pdcc/p2p/" + std::to_string(lo) + ":" + std::to_string(hi),
+                     prank = rank_ == lo ? 0 : 1, dev = ds.device, pi] {
+          pair_builder(pc, store, key, prank, dev, pi);
+        }).detach();
+      }
+      if (cfg_.watchdog_ms > 0) {
+        std::lock_guard<std::mutex> wl(wd_mu_);
+        inflight_.emplace_back(work);
+      }
+      record(cname, "rccl_pair_deferred", t.nbytes(), t0);
+      return work;
+    }
+  }
   auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, pi, rc.get(), s));
-    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, pi, rc.get(), s));
+    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
     if (!is_send && !w.is_same(t)) t.copy_(w);
-  });
+  }, nullptr, &pc->stream);
   record(cname, "rccl_pair", t.nbytes(), t0);
   return work;
+}
+
+// Builder thread of a PairChan: create the 2-rank communicator (blocking on the peer),
+// then enqueue the ops that queued up meanwhile, in order, each after its caller's
+// stream point, and open their gates; then mark the channel ready.
+void ProcessGroupMI355X::pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store,
+                                      std::string key, int prank, int dev, int pi) {
+  std::string err;
+  try {
+    PDCC_HIP(hipSetDevice(dev));
+    const auto t0 = std::chrono::steady_clock::now();
+    auto c = std::make_shared<RcclComm>(store, key, prank, 2, dev, RcclOpts());
+    std::lock_guard<std::mutex> lk(pc->mu);
+    pc->comm = c;
+    pc->init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  } catch (const std::exception& e) {
+    err = e.what();
+  }
+  for (;;) {
+    PairChan::Op op;
+    {
+      std::lock_guard<std::mutex> lk(pc->mu);
+      if (!err.empty()) pc->error = err;
+      if (pc->q.empty()) {
+        pc->ready = pc->error.empty();
+        return;
+      }
+      op = std::move(pc->q.front());
+      pc->q.pop_front();
+    }
+    try {
+      if (!err.empty()) throw std::runtime_error(err);
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(pc->stream);
+      const hipStream_t s = pc->stream.stream();
+      PDCC_HIP(hipStreamWaitEvent(s, op.after, 0));
+      if (op.is_send) PDCC_NCCL(ncclSend(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+      else PDCC_NCCL(ncclRecv(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+      if (!op.is_send && !op.w.is_same(op.t)) op.t.copy_(op.w);
+      for (const at::Tensor* x : {&op.t, &op.w})
+        c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(x->storage().data_ptr(),
+                                                                                         pc->stream);
+      PDCC_HIP(hipEventRecord(op.gate->ev, s));
+      op.gate->state.store(1, std::memory_order_release);
+    } catch (const std::exception& e) {
+      if (err.empty()) err = e.what();
+      std::lock_guard<std::mutex> lk(op.gate->mu);
+      op.gate->error = std::string("send/recv channel setup failed: ") + e.what();
+      op.gate->state.store(-1, std::memory_order_release);
+    }
+    (void)hipEventDestroy(op.after);
+  }
 }
 
 void ProcessGroupMI355X::startCoalescing() {

@@ -48,8 +48,12 @@ WorkMI355X::WorkMI355X(int rank, c10d::OpType type, uint64_t seq, std::vector<at
       pool_(std::move(pool)),
       comm_(comm) {}
 
+Gate::~Gate() {
+  if (ev) (void)hipEventDestroy(ev);
+}
+
 WorkMI355X::~WorkMI355X() {
-  if (!ev_) return;
+  if (!ev_ || gate_) return;  // a gated work's event belongs to its gate
   if (pool_) pool_->put(ev_);  // re-recording a pooled event later is fine: nobody waits on this one any more
   else hipEventDestroy(ev_);
 }
@@ -71,6 +75,12 @@ c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() {
   std::unique_lock<std::mutex> lk(mutex_);
   if (fut_) return fut_;
   if (gpu_) {
+    if (gate_) {  // the future's events go on the comm stream: the op must be there first
+      lk.unlock();
+      wait_gate(timeout_);
+      lk.lock();
+      if (fut_) return fut_;
+    }
     fut_ = c10::make_intrusive<c10::ivalue::Future>(c10::ListType::create(c10::TensorType::get()),
                                                     std::vector<c10::Device>{dev_});
     auto f = fut_;
@@ -141,7 +151,34 @@ void WorkMI355X::fail(const std::string& msg) {
   if (!exception_) exception_ = std::make_exception_ptr(std::runtime_error(msg));
 }
 
+bool WorkMI355X::gate_open() {
+  if (!gate_) return true;
+  const int st = gate_->state.load(std::memory_order_acquire);
+  if (st == 0) return false;
+  if (st < 0) {
+    std::lock_guard<std::mutex> lk(gate_->mu);
+    throw std::runtime_error("pdcc: " + gate_->error);
+  }
+  return true;
+}
+
+void WorkMI355X::wait_gate(std::chrono::milliseconds lim) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!gate_open()) {
+    check_health();
+    if (std::chrono::steady_clock::now() - t0 > lim)
+      throw std::runtime_error("pdcc: Work.wait() timed out after " + std::to_string(lim.count()) +
+                               " ms waiting for the point-to-point channel to be set up");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
 bool WorkMI355X::gpu_event_done() {
+  if (gate_) {
+    const int st = gate_->state.load(std::memory_order_acquire);
+    if (st == 0) return false;
+    if (st < 0) return true;
+  }
   if (done_word_) return __atomic_load_n(done_word_, __ATOMIC_ACQUIRE) >= done_value_;
   if (!ev_) return true;
   return hipEventQuery(ev_) == hipSuccess;
@@ -166,12 +203,14 @@ bool WorkMI355X::isCompleted() {
 bool WorkMI355X::isSuccess() const {
   if (!gpu_) return c10d::Work::isSuccess();
   if (health_ && health_->poisoned.load()) return false;
+  if (gate_ && gate_->state.load() < 0) return false;
   std::lock_guard<std::mutex> lk(mutex_);
   return !exception_;
 }
 
 void WorkMI355X::synchronize() {
   if (!gpu_) return;
+  wait_gate(timeout_);
   c10::hip::HIPGuardMasqueradingAsCUDA g(dev_);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(dev_.index());
   if (comm_ && *comm_ == cur) return;  // enqueued on this very stream: already ordered
@@ -363,7 +402,10 @@ ProcessGroupMI355X::~ProcessGroupMI355X() {
     DeviceState& ds = *kv.second;
     if (!health_->poisoned.load()) continue;
     if (ds.rccl) ds.rccl->abort();
-    for (auto& p : ds.pair_rccl) p.second->abort();
+    for (auto& p : ds.pairs) {
+      std::lock_guard<std::mutex> lk(p.second->mu);
+      if (p.second->comm) p.second->comm->abort();
+    }
   }
 }
 
@@ -557,7 +599,10 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
     for (auto& kv : devs_) {
       DeviceState& ds = *kv.second;
       if (ds.rccl) ds.rccl->abort();
-      for (auto& p : ds.pair_rccl) p.second->abort();
+      for (auto& p : ds.pairs) {
+        std::lock_guard<std::mutex> plk(p.second->mu);
+        if (p.second->comm) p.second->comm->abort();
+      }
       if (ds.ipc) ds.ipc->abort();  // kernels spinning in a cross-GPU barrier leave it
     }
     if (shm_) shm_->abort();
@@ -632,10 +677,13 @@ void ProcessGroupMI355X::watchdog_loop() {
     std::lock_guard<std::mutex> lk(init_mu_);
     for (auto& kv : devs_) {
       DeviceState& ds = *kv.second;
-      std::vector<RcclComm*> comms;
-      if (ds.rccl) comms.push_back(ds.rccl.get());
-      for (auto& p : ds.pair_rccl) comms.push_back(p.second.get());
-      for (RcclComm* c : comms) {
+      std::vector<std::shared_ptr<RcclComm>> comms;
+      if (ds.rccl) comms.push_back(ds.rccl);
+      for (auto& p : ds.pairs) {
+        std::lock_guard<std::mutex> plk(p.second->mu);
+        if (p.second->comm) comms.push_back(p.second->comm);
+      }
+      for (auto& c : comms) {
         ncclResult_t r = c->async_error();
         if (r != ncclSuccess && r != ncclInProgress) {
           const std::string m = std::string("RCCL async error: ") + ncclGetErrorString(r);

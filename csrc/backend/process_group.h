@@ -85,6 +85,17 @@ struct StreamSync {
   ~StreamSync();
 };
 
+// Completion gate of a GPU work whose enqueue is deferred to another thread (the
+// first point-to-point ops of a pair, queued behind its communicator's creation):
+// 0 = not enqueued yet, 1 = enqueued (then `ev` is recorded), -1 = failed.
+struct Gate {
+  std::atomic<int> state{0};
+  hipEvent_t ev = nullptr;  // owned: recorded by the enqueuing thread after the op
+  std::mutex mu;
+  std::string error;
+  ~Gate();
+};
+
 class WorkMI355X : public c10d::Work {
  public:
   // completed (or failed) CPU work
@@ -111,6 +122,8 @@ class WorkMI355X : public c10d::Work {
     done_word_ = word;
     done_value_ = value;
   }
+  // GPU work enqueued later by another thread: `gate->ev` is this work's event
+  void set_gate(std::shared_ptr<Gate> g) { gate_ = std::move(g); }
   void done(std::exception_ptr e);  // CPU async completion
   bool gpu() const { return gpu_; }
   bool gpu_event_done();
@@ -120,6 +133,10 @@ class WorkMI355X : public c10d::Work {
 
  private:
   void check_health();
+  // deferred enqueue: false while the op is not on its stream yet; throws if it failed
+  bool gate_open();
+  void wait_gate(std::chrono::milliseconds lim);
+  std::shared_ptr<Gate> gate_;
   uint64_t seq_;
   bool gpu_ = false;
   std::vector<at::Tensor> outputs_;
@@ -140,6 +157,31 @@ class WorkMI355X : public c10d::Work {
   c10::intrusive_ptr<c10::ivalue::Future> fut_;
 };
 
+// Point-to-point channel to one peer on another GPU: a 2-rank RCCL communicator
+// and a stream of its own, so the send to `next` and the recv from `prev` of a
+// ring never queue behind each other (ProcessGroupNCCL keys its p2p communicators
+// and streams by pair the same way). The communicator is built on a thread of its
+// own; ops issued before it is ready queue behind it in order, and their works'
+// gates open once they are enqueued -- so a ring of FIRST isends, which would
+// deadlock on blocking pairwise initialisation, never blocks a caller.
+struct PairChan {
+  std::mutex mu;
+  c10::hip::HIPStreamMasqueradingAsCUDA stream;
+  std::shared_ptr<RcclComm> comm;
+  bool ready = false;    // communicator built and queue drained: issue directly
+  bool started = false;  // builder thread running
+  std::string error;
+  double init_ms = 0.0;
+  struct Op {
+    bool is_send;
+    at::Tensor t, w;
+    hipEvent_t after;  // recorded on the caller's stream when the op was issued
+    std::shared_ptr<Gate> gate;
+  };
+  std::deque<Op> q;
+  explicit PairChan(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
+};
+
 struct DeviceState {
   int device = -1;
   c10::hip::HIPStreamMasqueradingAsCUDA stream;  // comm stream for async collectives (PDCC_STREAM)
@@ -152,8 +194,8 @@ struct DeviceState {
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
   std::shared_ptr<IpcComm> ipc;         // lazy
-  std::map<int, std::shared_ptr<RcclComm>> pair_rccl;  // 2-rank communicators for send/recv, by peer
-  std::map<int, bool> pair_distinct;                   // peer on another device (RCCL-capable pair)?
+  std::map<int, std::shared_ptr<PairChan>> pairs;  // send/recv channels to peers on other GPUs
+  std::map<int, bool> pair_distinct;               // peer on another device (RCCL-capable pair)?
   std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
   std::shared_ptr<StreamSync> sync = std::make_shared<StreamSync>();
   explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
@@ -253,7 +295,9 @@ class ProcessGroupMI355X : public c10d::Backend {
   DeviceState& dev_state(const at::Tensor& t);
   void init_topology(DeviceState& ds);
   RcclComm& rccl(DeviceState& ds);
-  RcclComm& rccl_pair(DeviceState& ds, int peer);
+  std::shared_ptr<PairChan> pair_chan(DeviceState& ds, int peer);
+  static void pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store, std::string key,
+                           int prank, int dev, int pi);
   bool pair_on_distinct_devices(DeviceState& ds, int peer);
   IpcComm& ipc(DeviceState& ds);
   RcclOpts rccl_opts() const;
@@ -272,7 +316,8 @@ class ProcessGroupMI355X : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> gpu_run(Coll c, DeviceState& ds, const std::vector<at::Tensor>& keep_alive,
                                          std::vector<at::Tensor> outputs, std::chrono::milliseconds timeout,
                                          const std::function<void(hipStream_t)>& fn,
-                                         std::shared_ptr<IpcComm> ipc = nullptr);
+                                         std::shared_ptr<IpcComm> ipc = nullptr,
+                                         const c10::hip::HIPStreamMasqueradingAsCUDA* stream = nullptr);
   c10::intrusive_ptr<c10d::Work> cpu_done(Coll c, std::vector<at::Tensor> outputs);
   // GPU tensors through the host transport (D2H, shm, H2D); synchronous
   c10::intrusive_ptr<c10d::Work> host_staged(Coll c, std::vector<at::Tensor> outputs,

@@ -488,7 +488,7 @@ def autotune_all_colls(rank, size, device="cuda", n=1 << 16):
     out = torch.empty(n * size, device=d)
     dist.all_gather_into_tensor(out, base + rank)
     ok["all_gather_flat"] = all(bool(torch.equal(out[r * n:(r + 1) * n], base + r)) for r in range(size))
-    lst = [torch.empty(n, device=d) for _ in range(size)]
+    lst = [torch.empty(n + 64, device=d)[:n] for _ in range(size)]  # gaps: never adjacent views
     dist.all_gather(lst, base + rank)
     ok["all_gather_list"] = all(bool(torch.equal(lst[r], base + r)) for r in range(size))
     glist = [torch.empty(n, device=d) for _ in range(size)] if rank == 0 else None
