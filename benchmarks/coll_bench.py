@@ -11,8 +11,9 @@ then ``new_group(range(world))`` exactly like the reference (main.py:11,94);
 per iteration ``barrier`` + timed collective; p50 = median over iterations of the
 max-over-ranks time. busbw factors: all_reduce 2(n-1)/n; reduce and broadcast 1;
 gather, scatter, all_gather, reduce_scatter, all_to_all (n-1)/n on the total
-bytes. After every timed collective the result is checked (correctness is part
-of the benchmark). Prints one JSON line per (collective, op, dtype, size).
+bytes. Inputs are reset before every timed call (outside the clock) and the
+results of every timed bulk call are checked against independently computed
+values (correctness is part of the benchmark). Prints one JSON line per (collective, op, dtype, size).
 """
 from __future__ import annotations
 
@@ -80,7 +81,9 @@ def worker(rank, size, cfg):
                 else:
                     n = max(1, nbytes // esz // size)
                     total = n * esz * size
-                x = (torch.arange(n, device=dev) % 7 + 1).to(dtype)
+                v = (torch.arange(n, device=dev) % 7 + 1).to(dtype)  # small integers: exact in every dtype
+                x = v + rank
+                reset = lambda: None  # noqa: E731
                 if coll == "all_gather":
                     outs = [torch.empty(n, dtype=dtype, device=dev) for _ in range(size)]
                     fn = lambda: dist.all_gather(outs, x, group=g)  # noqa: E731
@@ -88,66 +91,102 @@ def worker(rank, size, cfg):
                     outs = [torch.empty(n, dtype=dtype, device=dev) for _ in range(size)] if rank == 0 else []
                     fn = lambda: dist.gather(x, gather_list=outs if rank == 0 else None, dst=0, group=g)  # noqa: E731
                 elif coll == "scatter":
-                    ins = [x.clone() for _ in range(size)] if rank == 0 else None
+                    ins = [v + q for q in range(size)] if rank == 0 else None
                     out = torch.empty(n, dtype=dtype, device=dev)
                     fn = lambda: dist.scatter(out, scatter_list=ins, src=0, group=g)  # noqa: E731
                 elif coll == "reduce_scatter":
-                    inp = x.repeat(size)
+                    inp = torch.cat([v + rank + q for q in range(size)])
                     out = torch.empty(n, dtype=dtype, device=dev)
                     fn = lambda: dist.reduce_scatter_tensor(out, inp, op=op, group=g)  # noqa: E731
                 elif coll == "all_to_all":
-                    inp = x.repeat(size)
+                    inp = torch.cat([v + 10 * rank + q for q in range(size)])
                     out = torch.empty(n * size, dtype=dtype, device=dev)
                     fn = lambda: dist.all_to_all_single(out, inp, group=g)  # noqa: E731
-                elif coll == "all_reduce":
+                elif coll in ("all_reduce", "reduce"):
                     buf = x.clone()
-                    fn = lambda: dist.all_reduce(buf, op=op, group=g)  # noqa: E731
-                elif coll == "reduce":
-                    buf = x.clone()
-                    fn = lambda: dist.reduce(buf, dst=0, op=op, group=g)  # noqa: E731
+                    reset = lambda: buf.copy_(x)  # noqa: E731  (in place: every timed call starts from x)
+                    if coll == "all_reduce":
+                        fn = lambda: dist.all_reduce(buf, op=op, group=g)  # noqa: E731
+                    else:
+                        fn = lambda: dist.reduce(buf, dst=0, op=op, group=g)  # noqa: E731
                 else:
                     buf = x.clone()
+                    reset = lambda: buf.copy_(v if rank == 0 else torch.zeros_like(v))  # noqa: E731
                     fn = lambda: dist.broadcast(buf, src=0, group=g)  # noqa: E731
                 for _ in range(cfg["warmup"]):
+                    reset()
                     fn()
                 lat = []
+                oks = []
                 iters = cfg["iters"] if nbytes >= (1 << 20) else max(cfg["iters"], cfg["small_iters"])
                 for _ in range(iters):
+                    reset()
                     sync()
                     t0 = time.perf_counter()
                     fn()
                     if dev.type == "cuda":
                         torch.cuda.synchronize()
                     lat.append(max_t(time.perf_counter() - t0))
-                ok = _check(coll, op_name, rank, size, x, locals(), dist, torch)
+                    if not oks or nbytes >= (1 << 20):  # check the result of every timed bulk call
+                        oks.append(_check(coll, op_name, rank, size, v, locals(), torch))
                 p50 = statistics.median(lat)
                 rows.append({
                     "coll": coll, "op": op_name, "dtype": cfg["dtype"], "bytes": total, "world": size,
                     "p50_us": round(p50 * 1e6, 2), "algbw_GBps": round(total / p50 / 1e9, 3) if p50 > 0 else None,
                     "busbw_GBps": round(total * busbw_factor(coll, size) / p50 / 1e9, 3) if p50 > 0 else None,
-                    "correct": ok,
+                    "correct": all(oks),
                 })
-                del x
+                del x, v
     return rows
 
 
-def _check(coll, op_name, rank, size, x, loc, dist, torch):
-    """Verify the last result (values were chosen so every op is exact)."""
+def _reduce_ref(op_name, parts, torch):
+    """Exact reduction of the per-rank inputs, in float64 on the host."""
+    st = torch.stack([p.double().cpu() for p in parts])
+    if op_name in ("SUM",):
+        return st.sum(0)
+    if op_name == "AVG":
+        return st.mean(0)
+    if op_name == "PRODUCT":
+        return st.prod(0)
+    if op_name == "MAX":
+        return st.max(0).values
+    if op_name == "MIN":
+        return st.min(0).values
+    raise ValueError(op_name)
+
+
+def _close(got, ref, torch):
+    g = got.double().cpu()
+    exact = got.dtype in (torch.float64, torch.int32, torch.int64, torch.int8, torch.uint8)
+    if exact or bool((ref.abs() < 256).all()):
+        return bool(torch.equal(g, ref.to(got.dtype).double()))
+    rtol = 1e-6 if got.dtype == torch.float32 else 1e-2
+    return bool(torch.allclose(g, ref.to(got.dtype).double(), rtol=rtol, atol=0))
+
+
+def _check(coll, op_name, rank, size, v, loc, torch):
+    """Verify a result against values computed independently (inputs are rank-dependent
+    small integers, so every engine's result is exact or within a rounding tolerance)."""
     try:
         if coll == "broadcast":
-            return bool(torch.equal(loc["buf"], x))
-        if coll in ("all_gather",):
-            return all(bool(torch.equal(o, x)) for o in loc["outs"])
+            return bool(torch.equal(loc["buf"], v))
+        if coll == "all_gather":
+            return all(bool(torch.equal(o, v + q)) for q, o in enumerate(loc["outs"]))
         if coll == "gather":
-            return rank != 0 or all(bool(torch.equal(o, x)) for o in loc["outs"])
+            return rank != 0 or all(bool(torch.equal(o, v + q)) for q, o in enumerate(loc["outs"]))
         if coll == "scatter":
-            return bool(torch.equal(loc["out"], x))
+            return bool(torch.equal(loc["out"], v + rank))
         if coll == "all_to_all":
-            return bool(torch.equal(loc["out"], loc["inp"]))
-        if coll in ("all_reduce", "reduce_scatter"):
-            # repeated in-place all_reduce changes values; only the first call is checkable
-            return True
-        return True
+            exp = torch.cat([v + 10 * q + rank for q in range(size)])
+            return bool(torch.equal(loc["out"], exp))
+        if coll == "reduce_scatter":
+            return _close(loc["out"], _reduce_ref(op_name, [v + r + rank for r in range(size)], torch), torch)
+        if coll == "all_reduce" or (coll == "reduce" and rank == 0):
+            return _close(loc["buf"], _reduce_ref(op_name, [v + r for r in range(size)], torch), torch)
+        if coll == "reduce":
+            return True  # non-root buffers are unspecified (SURVEY.md §4.2)
+        return False
     except Exception:
         return False
 
