@@ -258,7 +258,7 @@ def run_rank(args):
 
     extras = {}
     if args.extras and on_gpu:
-        timer = threading.Timer(float(os.environ.get("PDCC_BENCH_EXTRAS_S", "300")), deadline, args=("extras",))
+        timer = threading.Timer(float(os.environ.get("PDCC_BENCH_EXTRAS_S", "240")), deadline, args=("extras",))
         timer.daemon = True
         timer.start()
         try:
@@ -377,7 +377,83 @@ def run_extras(world, rank, dev, native, x):
         except Exception as e:
             out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
         out.update(graph_replay(world, rank, dev))
+        try:
+            out["rccl_tuning"] = rccl_tuning(world, rank, dev, x)
+        except Exception as e:
+            out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
     return out
+
+
+def _group_with_env(world, env, timeout_s=60):
+    """A new full group whose backend reads `env` at construction (PDCC_* knobs are
+    per group), built with a fresh RCCL communicator so per-communicator settings
+    (channel bounds) take effect."""
+    import torch.distributed as dist
+
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return dist.new_group(list(range(world)), timeout=datetime.timedelta(seconds=timeout_s))
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def rccl_tuning(world, rank, dev, x):
+    """RCCL on this node's xGMI (only where ranks sit on distinct GPUs):
+    * cta_sweep: 1 GiB all_reduce busbw for RCCL channel floors (minCTAs) default/7/14/28
+      -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate;
+    * list_all_gather: all_gather into separate tensors, grouped p2p straight into the
+      list (zero copy) vs ring all_gather into staging + K2 unpack;
+    * group_churn: new_group(range(n)) + first all_reduce, as every reference demo does."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+    from pytorch_distributed_collective_communication_amd.utils import busbw as bb
+
+    if "rccl_ok=1" not in be.native_backend(None, "cuda").describe():
+        return {"skipped": "ranks share a GPU: RCCL unavailable"}
+    res = {}
+    big = x if not SMALL else x[: (64 << 20) // 4]
+    sweep = {}
+    for ctas in ("default", 7, 14, 28):
+        progress(f"rccl cta sweep: {ctas}")
+        env = {"PDCC_RCCL_GROUP_COMM": "init", "PDCC_ALGO": "rccl"}
+        if ctas != "default":
+            env["PDCC_RCCL_MIN_CTAS"] = ctas
+        g = _group_with_env(world, env)
+        t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
+        sweep[str(ctas)] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
+        dist.destroy_process_group(g)
+    res["cta_sweep_allreduce_busbw"] = sweep
+    per = ((256 << 20) if not SMALL else (16 << 20)) // 4
+    src = torch.full((per,), float(rank), device=dev)
+    for mode in ("p2p", "staged"):
+        progress(f"list all_gather: {mode}")
+        g = _group_with_env(world, {"PDCC_LIST_GATHER": mode, "PDCC_ALGO": "rccl"})
+        outs = [torch.empty(per + 64, device=dev)[:per] for _ in range(world)]  # never adjacent
+        t = _p50_coll(lambda: dist.all_gather(outs, src, group=g), iters=5)
+        ok = all(bool(outs[r][0].item() == r and outs[r][-1].item() == r) for r in range(world))
+        res[f"list_all_gather_{mode}"] = {"per_rank_bytes": per * 4, "p50_ms": round(t * 1e3, 3),
+                                          "busbw_GBps": round(bb("all_gather", per * 4 * world, world, t), 1),
+                                          "correct": ok}
+        del outs
+        dist.destroy_process_group(g)
+    churn = []
+    for _ in range(3):
+        dist.barrier()
+        t0 = time.perf_counter()
+        g = dist.new_group(list(range(world)))
+        y = torch.ones(1024, device=dev)
+        dist.all_reduce(y, group=g)
+        torch.cuda.synchronize()
+        churn.append(round((time.perf_counter() - t0) * 1e3, 2))
+    res["group_churn_ms"] = churn
+    return res
 
 
 def graph_replay(world, rank, dev, n_ops=16, numel=1024):

@@ -109,6 +109,7 @@ Config Config::from_env() {
   if (c.rccl_min_ctas > 0 && c.rccl_max_ctas > 0 && c.rccl_min_ctas > c.rccl_max_ctas)
     throw std::runtime_error("PDCC_RCCL_MIN_CTAS must not exceed PDCC_RCCL_MAX_CTAS");
   c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
+  c.eager_init = env_bool("PDCC_EAGER_INIT", c.eager_init);
   if (const char* sm = env("PDCC_STREAM")) {
     std::string v(sm);
     if (v == "auto") c.stream_mode = 0;

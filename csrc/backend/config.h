@@ -63,6 +63,7 @@ struct Config {
   // into the list (zero copy), staged = ncclAllGather into a staging buffer + K2 unpack
   bool list_gather_p2p = true;             // PDCC_LIST_GATHER=p2p|staged
   bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
+  bool eager_init = false;                 // PDCC_EAGER_INIT=1: GPU setup at group construction
   // host transport
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES
   size_t shm_chan_bytes = 1u << 20;        // PDCC_SHM_CHAN_BYTES

@@ -241,8 +241,9 @@ std::string ProcessGroupMI355X::make_members_key(const std::vector<int64_t>& glo
 }
 
 // =================================================================== device state
-DeviceState& ProcessGroupMI355X::dev_local(const at::Tensor& t) {
-  const int d = t.device().index();
+DeviceState& ProcessGroupMI355X::dev_local(const at::Tensor& t) { return dev_local_idx(t.device().index()); }
+
+DeviceState& ProcessGroupMI355X::dev_local_idx(int d) {
   std::lock_guard<std::mutex> lk(init_mu_);
   auto it = devs_.find(d);
   if (it != devs_.end()) return *it->second;
@@ -272,6 +273,19 @@ DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
   std::lock_guard<std::mutex> lk(init_mu_);
   if (!ds.topo) init_topology(ds);
   return ds;
+}
+
+// PDCC_EAGER_INIT=1: everything the first GPU collective would set up (topology,
+// IPC self-test, RCCL communicator) happens in init_process_group / new_group,
+// on the current device -- so the first collective is not the one paying for
+// it, and a graph can be captured right away.
+void ProcessGroupMI355X::eager_init(int device) {
+  DeviceState& ds = dev_local_idx(device);
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    if (!ds.topo) init_topology(ds);
+  }
+  if ((size_ > 1 || !cfg_.world1_local) && ds.rccl_ok) rccl(ds);
 }
 
 // Collective over the group (init_mu_ held): where is every rank, can RCCL run (one

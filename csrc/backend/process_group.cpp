@@ -386,6 +386,11 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
   }
   if (const char* fr = std::getenv("PDCC_FLIGHT_RECORDER")) fr_cap_ = (size_t)std::max(0, std::atoi(fr));
   if (cfg_.watchdog_ms > 0) wd_thr_ = std::thread([this] { watchdog_loop(); });
+  if (cfg_.eager_init) {
+    int n = 0, d = 0;
+    if (hipGetDeviceCount(&n) == hipSuccess && n > 0 && hipGetDevice(&d) == hipSuccess) eager_init(d);
+    else (void)hipGetLastError();
+  }
 }
 
 ProcessGroupMI355X::~ProcessGroupMI355X() {

@@ -273,6 +273,8 @@ class ProcessGroupMI355X : public c10d::Backend {
     return last_algo_;
   }
   void abort_group(const std::string& why);
+  // set up device state, topology and the RCCL communicator now (PDCC_EAGER_INIT)
+  void eager_init(int device);
   // runtime overrides (must be applied identically on every rank of the group)
   void set_algo(const std::string& a);
   void set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max);
@@ -291,6 +293,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   host::ShmComm& shm_pair(int peer);
   // device state without the group-wide topology exchange (non-collective)
   DeviceState& dev_local(const at::Tensor& t);
+  DeviceState& dev_local_idx(int device);
   // device state + topology (collective over the group on first use)
   DeviceState& dev_state(const at::Tensor& t);
   void init_topology(DeviceState& ds);

@@ -154,7 +154,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_algo", &pdcc::ProcessGroupMI355X::set_algo)
       .def("set_ipc_thresholds", &pdcc::ProcessGroupMI355X::set_ipc_thresholds, py::arg("one_shot_max") = -1,
            py::arg("two_shot_max") = -1, py::arg("copy_max") = -1)
-      .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>());
+      .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>())
+      .def("eager_init", &pdcc::ProcessGroupMI355X::eager_init, py::arg("device"),
+           py::call_guard<py::gil_scoped_release>());
 
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
         py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");

@@ -17,27 +17,27 @@ struct CopyArgs {
   int tail_idx[kern::kMaxCopyDescs];
 };
 
+// Tile g of the launch lives in descriptor j with prefix[j] <= g < prefix[j+1]. A
+// block visits its tiles in increasing order (and pipe_run asks for sources and
+// destinations in increasing order too), so each side keeps a monotonic cursor:
+// amortised O(1) uniform scalar steps per tile instead of a binary search.
 struct DescMap {
   const CopyArgs* a;
   size_t first, stride, total;
+  mutable int js = 0, jd = 0;  // descriptor cursors of the source and destination sides
   __device__ size_t count() const { return first < total ? (total - 1 - first) / stride + 1 : 0; }
-  __device__ void locate(size_t i, int& j, size_t& lt) const {
+  __device__ size_t advance(int& j, size_t i) const {
     const size_t g = first + i * stride;
-    int lo = 0, hi = a->n - 1;  // last j with prefix[j] <= g  (uniform scalar search)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (a->prefix[mid] <= g) lo = mid; else hi = mid - 1;
-    }
-    j = lo;
-    lt = g - a->prefix[lo];
+    while (a->prefix[j + 1] <= g) ++j;
+    return g - a->prefix[j];
   }
   __device__ const char* src(int, size_t i) const {
-    int j; size_t lt; locate(i, j, lt);
-    return (const char*)a->d[j].src + lt * kTile;
+    const size_t lt = advance(js, i);
+    return (const char*)a->d[js].src + lt * kTile;
   }
   __device__ char* dst(size_t i) const {
-    int j; size_t lt; locate(i, j, lt);
-    return (char*)a->d[j].dst + lt * kTile;
+    const size_t lt = advance(jd, i);
+    return (char*)a->d[jd].dst + lt * kTile;
   }
   __device__ size_t valid(size_t) const { return kTile; }
 };

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """K2 multi_copy tuning sweep (interleaved rounds in one process): grid cap x
-LDS-DMA ring depth for 64 x 4 MiB and 8 x 32 MiB lists, plus a 1 GiB torch
-copy as the HBM reference. Bandwidth = 2 x bytes / time."""
+LDS-DMA ring depth for several list shapes, plus the default policy
+(max_blocks=0) and a torch copy of the same bytes as the HBM reference.
+Bandwidth = 2 x bytes / time (read + write)."""
 import json
 import os
 import statistics
@@ -26,24 +27,32 @@ def timeit(fn, iters=8):
 
 dev = torch.device("cuda", 0)
 out = {}
-for count, mib in ((64, 4), (8, 32)):
-    n = (mib << 20) // 4
+shapes = [(64, 4 << 20), (8, 32 << 20), (8, 1 << 20), (4, 256 << 20), (32, 64 << 10), (8, 128 << 20)]
+for count, nbytes in shapes:
+    n = nbytes // 4
+    tag = f"{count}x{nbytes >> 10}K"
     srcs = [torch.rand(n, device=dev) for _ in range(count)]
     dsts = [torch.empty_like(s) for s in srcs]
-    byts = 2 * count * n * 4
+    flat_src = torch.cat(srcs)
+    flat_dst = torch.empty_like(flat_src)
+    byts = 2 * count * nbytes
     res = {}
-    for _ in range(4):
+    for _ in range(3):
         for depth in (4, 8):
             for g in (256, 512, 1024, 2048):
                 t = timeit(lambda: ops.multi_copy(srcs, dsts, max_blocks=g, depth=depth))
-                res.setdefault(f"{count}x{mib}M_d{depth}_g{g}", []).append(byts / t / 1e9)
+                res.setdefault(f"{tag}_d{depth}_g{g}", []).append(byts / t / 1e9)
+        t = timeit(lambda: ops.multi_copy(srcs, dsts))
+        res.setdefault(f"{tag}_default", []).append(byts / t / 1e9)
+        t = timeit(lambda: flat_dst.copy_(flat_src))
+        res.setdefault(f"{tag}_torch_flat_copy", []).append(byts / t / 1e9)
     ok = all(torch.equal(a, b) for a, b in zip(srcs, dsts))
     for k, v in res.items():
         out[k] = round(statistics.median(v), 1)
-    out[f"{count}x{mib}M_correct"] = ok
-    del srcs, dsts
-big = torch.rand(1 << 28, device=dev)
-bd = torch.empty_like(big)
-out["torch_copy_1GiB"] = round(statistics.median([2 * big.numel() * 4 / timeit(lambda: bd.copy_(big)) / 1e9
-                                                  for _ in range(4)]), 1)
+    best = max((k for k in res if "_d" in k), key=lambda k: out[k])
+    out[f"{tag}_best"] = best
+    out[f"{tag}_default_vs_best"] = round(out[f"{tag}_default"] / out[best], 3)
+    out[f"{tag}_correct"] = ok
+    del srcs, dsts, flat_src, flat_dst
+    torch.cuda.empty_cache()
 print(json.dumps(out))

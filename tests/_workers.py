@@ -750,3 +750,17 @@ def engine_crosscheck(rank, size, device="cuda"):
         ok[f"max_{n}"] = bool(torch.equal(res["rccl"][1], res["ipc"][1]))
         ok[f"all_gather_{n}"] = bool(torch.equal(res["rccl"][2], res["ipc"][2]))
     return ok
+
+
+def eager_probe(rank, size, device="cuda"):
+    """PDCC_EAGER_INIT=1: the RCCL communicator exists right after
+    init_process_group (before the first collective), and collectives work."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    before = sorted(k for k in be.native_backend(None, "cuda").stats() if k.startswith("rccl_comm/"))
+    x = torch.full((4096,), float(rank + 1), device=_dev(device))
+    dist.all_reduce(x)
+    return {"before": before, "ok": bool(torch.all(x == size * (size + 1) / 2))}

@@ -161,6 +161,11 @@ def test_autotuner_every_collective_shared_gpu():
         assert e["ipc_valid"] and e["algo"] in ("ipc", "host"), e
 
 
+def test_eager_init_builds_the_communicator_up_front():
+    res = _gpu_launch(W.eager_probe, 1, env={"PDCC_WORLD1_LOCAL": "0", "PDCC_EAGER_INIT": "1"})[0]
+    assert res["ok"] and res["before"] == ["rccl_comm/init"], res
+
+
 @pytest.mark.parametrize("mode", ["split", "share"])
 def test_group_churn_reuses_the_communicator(mode):
     # main.py builds new_group(range(size)) in every demo: with PDCC_WORLD1_LOCAL=0 every
