@@ -90,6 +90,7 @@ Config Config::from_env() {
     }
   }
   c.ipc_spin_ms = (int64_t)env_size("PDCC_IPC_SPIN_MS", (size_t)c.ipc_spin_ms);
+  c.autotune_spin_ms = (int64_t)env_size("PDCC_AUTOTUNE_SPIN_MS", (size_t)c.autotune_spin_ms);
   if (const char* gc = env("PDCC_RCCL_GROUP_COMM")) {
     std::string v(gc);
     if (v == "split") c.group_comm = 0;

@@ -40,6 +40,10 @@ struct Config {
   // caller's data): above it both engines are bandwidth-bound, so the sample decides the bucket.
   size_t autotune_sample = 1ull << 30;     // PDCC_AUTOTUNE_SAMPLE
   uint32_t autotune_colls = 0xffffffffu;   // PDCC_AUTOTUNE_COLLS=allreduce,reduce,... (default all)
+  // Cross-GPU barrier spin bound while tuning: an IPC run that cannot finish (a topology
+  // the protocol fails on at this size) costs this much once, disqualifies IPC for the key
+  // and leaves the group healthy, instead of hanging for the group timeout.
+  int64_t autotune_spin_ms = 10000;        // PDCC_AUTOTUNE_SPIN_MS
   // PDCC_STREAM: auto (default) = synchronous collectives (async_op=False) on the caller's stream,
   // async ones on a normal-priority comm stream; high = auto with a high-priority comm stream;
   // comm = always the comm stream; current = always the caller's stream.

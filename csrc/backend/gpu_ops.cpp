@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstring>
 #include <sstream>
+#include <thread>
 
 #include "../device/comm_util.h"
 #include "process_group.h"
@@ -729,18 +730,62 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     PDCC_HIP(hipEventElapsedTime(&ms, a, b));
     return 1e3 * (double)ms;
   };
+  // IPC runs of the race get a short spin bound: a run that cannot complete here
+  // disqualifies IPC for this key (below) instead of hanging the group
+  struct Spin {
+    IpcComm* ic;
+    uint64_t saved;
+    std::atomic<bool>& flag;
+    Spin(IpcComm* c, uint64_t ms, std::atomic<bool>& f) : ic(c), saved(c ? c->timeout_ms() : 0), flag(f) {
+      flag.store(true);
+      if (ic) ic->set_timeout_ms(std::max<uint64_t>(1, std::min<uint64_t>(ms, saved)));
+    }
+    ~Spin() {
+      if (ic) ic->set_timeout_ms(saved);
+      flag.store(false);
+    }
+  };
+  bool has_ipc = false;
+  for (Algo a : cands) has_ipc = has_ipc || a == Algo::IPC;
+  Spin spin(has_ipc ? ds.ipc.get() : nullptr, (uint64_t)cfg_.autotune_spin_ms, tuning_);
   // 0) warm-up: one run each (staging growth, first-touch), then check every result
   //    against the reference engine's on identical data
-  for (size_t k = 0; k < n; ++k) run(k);
+  for (size_t k = 0; k < n; ++k) {
+    if (cands[k] == Algo::IPC)
+      if (const char* d = std::getenv("PDCC_TEST_AUTOTUNE_DELAY"))  // test hook "rank:ms": a late peer
+        if (std::atoi(d) == rank_) {
+          PDCC_HIP(hipStreamSynchronize(s));
+          std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(std::strchr(d, ':') + 1)));
+        }
+    run(k);
+  }
   PDCC_HIP(hipStreamSynchronize(s));
   std::vector<double> v(2 * n, 0.0);  // [estimate_us x n, mismatch x n], MAX-reduced across ranks
-  for (size_t k = 1; k < n; ++k) v[n + k] = same(0, k) ? 0.0 : 1.0;
+  const bool ipc_fault = has_ipc && ds.ipc && ds.ipc->error_word() != 0;
+  for (size_t k = 1; k < n; ++k)
+    v[n + k] = (cands[k] == Algo::IPC && ipc_fault) ? 2.0 : (same(0, k) ? 0.0 : 1.0);
+  {  // agree on faults first (every rank's stream is drained: no IPC kernel is running)
+    std::vector<double> f(v.begin() + n, v.end());
+    shm().allreduce(f.data(), f.size(), at::kDouble, RedOpType::MAX, timeout_);
+    std::copy(f.begin(), f.end(), v.begin() + n);
+  }
+  std::vector<bool> live(n, true);
+  for (size_t k = 1; k < n; ++k)
+    if (v[n + k] >= 2.0) {
+      live[k] = false;  // an IPC barrier timed out on some rank: drop IPC from the race
+      if (ds.ipc) ds.ipc->clear_error();
+      fprintf(stderr, "[pdcc r%d] autotune %s %zu B: IPC run timed out (>%lld ms); using %s for this key\n", rank_,
+              coll_name((Coll)std::get<0>(key)), bytes, (long long)cfg_.autotune_spin_ms, algo_name(cands[0]));
+    }
+  const std::function<void(size_t)> run_live = [&](size_t k) {
+    if (live[k]) run(k);
+  };
   // 1) one timed run each: sizes the measurement (same count on every rank: MAX-reduced inputs)
   std::vector<hipEvent_t> e1(n + 1);
   for (auto& e : e1) PDCC_HIP(hipEventCreate(&e));
   PDCC_HIP(hipEventRecord(e1[0], s));
   for (size_t k = 0; k < n; ++k) {
-    run(k);
+    run_live(k);
     PDCC_HIP(hipEventRecord(e1[k + 1], s));
   }
   PDCC_HIP(hipEventSynchronize(e1[n]));
@@ -756,7 +801,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   PDCC_HIP(hipEventRecord(ev[0], s));
   for (int i = 0; i < iters; ++i)
     for (size_t k = 0; k < n; ++k) {
-      run(k);
+      run_live(k);
       PDCC_HIP(hipEventRecord(ev[i * n + k + 1], s));
     }
   PDCC_HIP(hipEventSynchronize(ev[iters * n]));
@@ -772,7 +817,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   shm().allreduce(med.data(), med.size(), at::kDouble, RedOpType::MAX, timeout_);
   size_t best = 0;
   for (size_t k = 1; k < n; ++k)
-    if (v[n + k] == 0.0 && med[k] < med[best]) best = k;
+    if (live[k] && v[n + k] == 0.0 && med[k] < med[best]) best = k;
   TuneEntry te;
   te.ref = cands[0];
   te.iters = iters;

@@ -698,7 +698,7 @@ void ProcessGroupMI355X::watchdog_loop() {
           if (ds.ipc) ds.ipc->abort();
         }
       }
-      if (ds.ipc && ds.ipc->error_word() != 0 && !health_->poisoned.load()) {
+      if (ds.ipc && ds.ipc->error_word() != 0 && !health_->poisoned.load() && !tuning_.load()) {
         const std::string m = "IPC collective timed out waiting for a peer (error word " +
                               std::to_string(ds.ipc->error_word()) + ")";
         fprintf(stderr, "[pdcc] rank %d: %s\n", rank_, m.c_str());

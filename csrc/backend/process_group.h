@@ -434,6 +434,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   using TuneKey = std::tuple<int, int, int, int>;
   std::map<TuneKey, TuneEntry> tune_;
   std::mutex tune_mu_;
+  std::atomic<bool> tuning_{false};  // an autotune race is running: IPC spin timeouts are its verdict
   // engines worth timing for this call (reference engine first); empty = no tuning
   std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const;
   Algo tuned(const TuneKey& k);

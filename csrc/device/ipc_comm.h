@@ -44,6 +44,7 @@ class IpcComm {
 
   // spin timeout of the cross-GPU barriers of later launches
   void set_timeout_ms(uint64_t ms) { timeout_ticks_ = ms * 100000ull; }
+  uint64_t timeout_ms() const { return timeout_ticks_ / 100000ull; }
   // a launch was captured into a graph: sequence numbers live on the device from now on
   bool graph_mode() const { return graph_mode_; }
 

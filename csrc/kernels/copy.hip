@@ -194,8 +194,18 @@ hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t
   return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, false);
 }
 
+// Default K2 grid from the launch's shape (scripts/k2_sweep.py on MI355X, profiles/README.md):
+// small lists are latency-bound and want one tile per workgroup; big streams want few,
+// long-running workgroups, and the fewer the larger the descriptors (each workgroup's
+// strided tiles then stay within one DRAM-friendly window): 256 workgroups from 16 MiB
+// per descriptor (8 x 32 MiB: 5.9 TB/s vs 4.9 at 1024), 512 below (64 x 4 MiB: 5.6 vs 5.1).
+static int k2_grid(uint64_t tiles, int ndesc, size_t bytes) {
+  if (tiles <= 4096) return (int)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 2048));
+  const size_t avg = bytes / (size_t)std::max(1, ndesc);
+  return avg >= (16u << 20) ? 256 : 512;
+}
+
 hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks, int depth) {
-  if (max_blocks <= 0) max_blocks = kK2Grid;
   if (depth <= 0) depth = kK2Depth;
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   for (int base = 0; base < n; base += kMaxCopyDescs) {
@@ -220,8 +230,9 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
     }
     if (a.n == 0) continue;
     a.prefix[a.n] = acc;
+    const int cap = max_blocks > 0 ? max_blocks : k2_grid(acc, a.n, bytes);
     const int grid =
-        (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), (uint64_t)max_blocks));
+        (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), (uint64_t)cap));
     if (depth >= 8) hipLaunchKernelGGL(dev::k2_multi_copy<8>, dim3(grid), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(dev::k2_multi_copy<4>, dim3(grid), dim3(256), 0, stream, a);
     hipError_t e = hipGetLastError();

@@ -62,10 +62,10 @@ struct CopyDesc {
   size_t bytes;
 };
 constexpr int kMaxCopyDescs = 64;  // per launch (kernarg); host splits longer lists
-constexpr int kK2Grid = 1024;      // K2 default grid cap (4 workgroups per CU: one LDS ring each)
 constexpr int kK2Depth = 4;        // K2 default LDS-DMA ring depth (tiles in flight per workgroup)
 // One launch copies every descriptor (pack = many->one, unpack = one->many).
-// max_blocks / depth: 0 = defaults (kK2Grid workgroups, kK2Depth tiles in flight per workgroup)
+// max_blocks / depth: 0 = defaults (grid from the list's shape, see k2_grid in copy.hip;
+// kK2Depth tiles in flight per workgroup)
 hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks = 0, int depth = 0);
 
 // ---------------------------------------------------------------- IPC collectives

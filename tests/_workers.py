@@ -764,3 +764,28 @@ def eager_probe(rank, size, device="cuda"):
     x = torch.full((4096,), float(rank + 1), device=_dev(device))
     dist.all_reduce(x)
     return {"before": before, "ok": bool(torch.all(x == size * (size + 1) / 2))}
+
+
+def autotune_fault_probe(rank, size, device="cuda"):
+    """An IPC run of the autotune race that times out on one rank (rank 1 arrives
+    late, PDCC_TEST_AUTOTUNE_DELAY) must disqualify IPC for that key only: the
+    call still returns the right sum, the group stays healthy, and later calls
+    (IPC included) work."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    x = torch.full((1 << 18,), float(rank + 1), device=d)  # 1 MiB: tuned bucket
+    dist.all_reduce(x)
+    ok = [bool(torch.all(x == size * (size + 1) / 2))]
+    b = be.native_backend(None, "cuda")
+    ok.append(b.healthy())
+    y = torch.full((1000,), float(rank), device=d)  # small: IPC 1-shot by the static threshold
+    dist.all_reduce(y)
+    ok.append(bool(torch.all(y == size * (size - 1) / 2)))
+    x.fill_(1.0)
+    dist.all_reduce(x)
+    ok.append(bool(torch.all(x == size)))
+    return {"ok": ok, "table": be.autotune_table()}

@@ -161,6 +161,15 @@ def test_autotuner_every_collective_shared_gpu():
         assert e["ipc_valid"] and e["algo"] in ("ipc", "host"), e
 
 
+def test_autotune_ipc_timeout_is_contained():
+    env = {"PDCC_TEST_AUTOTUNE_DELAY": "1:1500", "PDCC_AUTOTUNE_SPIN_MS": "300", "PDCC_AUTOTUNE_COLLS": "allreduce"}
+    res = _gpu_launch(W.autotune_fault_probe, 2, env=env)
+    for r in res:
+        assert all(r["ok"]), r
+    rows = [e for e in res[0]["table"] if e["lo"] == 1 << 20]
+    assert len(rows) == 1 and rows[0]["algo"] == "host" and not rows[0]["ipc_valid"], res[0]["table"]
+
+
 def test_eager_init_builds_the_communicator_up_front():
     res = _gpu_launch(W.eager_probe, 1, env={"PDCC_WORLD1_LOCAL": "0", "PDCC_EAGER_INIT": "1"})[0]
     assert res["ok"] and res["before"] == ["rccl_comm/init"], res
