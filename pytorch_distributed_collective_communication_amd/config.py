@@ -15,9 +15,18 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
 | PDCC_IPC_MAX_STAGING | 512M | staging bytes per parity; larger calls are chunked |
-| PDCC_AUTOTUNE | 1 | GPU all_reduce: time RCCL vs IPC on the first call per power-of-two size bucket (IPC result checked against RCCL's), adopt the faster on all ranks |
-| PDCC_AUTOTUNE_MIN / _MAX | 64K / 4G | size range the autotuner covers (outside: the static thresholds) |
+| PDCC_IPC_SPIN_MS | 600000 | bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if shorter) |
+| PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
+| PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
+| PDCC_AUTOTUNE_SAMPLE | 1G | bytes per engine the tuning runs move (a prefix of the caller's data) |
+| PDCC_AUTOTUNE_COLLS | all | comma list of collectives to tune (allreduce, reduce, broadcast, allgather, gather, scatter, reduce_scatter, alltoall) |
+| PDCC_AUTOTUNE_SPIN_MS | 10000 | spin bound of IPC runs during tuning; a timeout drops IPC for that key and keeps the group healthy |
 | PDCC_RCCL_MIN_CTAS / _MAX_CTAS | -1 / -1 | RCCL channel (CTA) bounds via ``ncclCommInitRankConfig``; -1 leaves RCCL's topology tuner in charge |
+| PDCC_RCCL_GROUP_COMM | share | groups with the same members as a live communicator: share it, split from it (ncclCommSplit) or init a fresh one |
+| PDCC_RCCL_SPLIT_SHARE | 1 | ncclCommSplit children share the parent's resources |
+| PDCC_RCCL_BUFFSIZE / _ALGO / _PROTO / _MIN_NCHANNELS / _MAX_NCHANNELS / _NTHREADS / _MSCCL / _MSCCLPP | unset | forwarded to NCCL_* / RCCL_* before the process's first communicator (the user's own NCCL_* setting wins) |
+| PDCC_LIST_GATHER | p2p | all_gather into separate tensors on RCCL: grouped send/recv into the list (p2p) or ring all_gather + K2 unpack (staged) |
+| PDCC_EAGER_INIT | 0 | build topology, IPC self-test and RCCL communicator when the group is created |
 | PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
@@ -30,6 +39,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_WATCHDOG_MS | 100 | watchdog poll period (0 disables timeout/abort handling) |
 | PDCC_FLIGHT_RECORDER | 256 | number of recent collectives kept for post-mortem dumps |
 | PDCC_FAULT | "" | fault injection ``rank:op_seq:kind`` (kind exit, raise, hang) |
+| PDCC_TEST_AUTOTUNE_DELAY | "" | test hook ``rank:ms``: that rank starts its IPC tuning run late |
 | PDCC_TAKEOVER_GLOO / _NCCL | 0 | serve ``init_process_group("gloo"/"nccl")`` with mi355x |
 """
 from __future__ import annotations
@@ -62,11 +72,19 @@ class Config:
     ipc_2shot_max: int = 8 << 20
     ipc_copy_max: int = 1 << 20
     ipc_max_staging: int = 512 << 20
+    ipc_spin_ms: int = 600000
     autotune: bool = True
     autotune_min: int = 64 << 10
-    autotune_max: int = 4 << 30
+    autotune_max: int = 1 << 42
+    autotune_sample: int = 1 << 30
+    autotune_colls: str = "all"
+    autotune_spin_ms: int = 10000
     rccl_min_ctas: int = -1
     rccl_max_ctas: int = -1
+    rccl_group_comm: str = "share"
+    rccl_split_share: bool = True
+    list_gather: str = "p2p"
+    eager_init: bool = False
     world1_local: bool = True
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
@@ -87,6 +105,10 @@ _ENV = {
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
+    "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
+    "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",
+    "rccl_group_comm": "PDCC_RCCL_GROUP_COMM", "rccl_split_share": "PDCC_RCCL_SPLIT_SHARE",
+    "list_gather": "PDCC_LIST_GATHER", "eager_init": "PDCC_EAGER_INIT",
     "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
     "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
@@ -115,6 +137,10 @@ def current(environ=None) -> Config:
         raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|host, got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
+    if c.rccl_group_comm not in ("share", "split", "init"):
+        raise ValueError(f"PDCC_RCCL_GROUP_COMM must be share|split|init, got {c.rccl_group_comm!r}")
+    if c.list_gather not in ("p2p", "staged"):
+        raise ValueError(f"PDCC_LIST_GATHER must be p2p|staged, got {c.list_gather!r}")
     return c
 
 
