@@ -616,6 +616,42 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
   for (auto& kv : shm_pairs_) kv.second->abort();
 }
 
+void ProcessGroupMI355X::abort() { abort_group("aborted by ProcessGroup.abort()"); }
+
+// Orderly shutdown (destroy_process_group): let enqueued GPU work drain for up to the
+// group timeout; a group that cannot drain (a peer is gone) is aborted instead of hanging.
+void ProcessGroupMI355X::shutdown() {
+  if (health_->poisoned.load()) return;
+  std::vector<hipStream_t> streams;
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    for (auto& kv : devs_) {
+      streams.push_back(kv.second->stream.stream());
+      for (auto& p : kv.second->pairs) streams.push_back(p.second->stream.stream());
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (hipStream_t s : streams) {
+    while (hipStreamQuery(s) == hipErrorNotReady) {
+      if (health_->poisoned.load()) return;
+      if (std::chrono::steady_clock::now() - t0 > timeout_) {
+        abort_group("shutdown: GPU work did not drain within the group timeout");
+        return;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    (void)hipGetLastError();
+  }
+}
+
+c10d::ErrorType ProcessGroupMI355X::getError() {
+  if (!health_->poisoned.load()) return c10d::ErrorType::SUCCESS;
+  const std::string m = health_->message();
+  if (m.find("timeout") != std::string::npos || m.find("timed out") != std::string::npos)
+    return c10d::ErrorType::TIMEOUT;
+  return c10d::ErrorType::COMM_ERROR;
+}
+
 void ProcessGroupMI355X::set_algo(const std::string& a) {
   if (a == "auto") cfg_.force_algo = Algo::AUTO;
   else if (a == "rccl") cfg_.force_algo = Algo::RCCL;

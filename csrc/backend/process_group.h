@@ -262,6 +262,12 @@ class ProcessGroupMI355X : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> recv(std::vector<at::Tensor>& tensors, int src, int tag) override;
   c10::intrusive_ptr<c10d::Work> barrier(const c10d::BarrierOptions& opts = c10d::BarrierOptions()) override;
 
+  // c10d lifecycle hooks: ProcessGroup.abort() / destroy_process_group() / _set_pg_timeout / error query
+  void abort() override;
+  void shutdown() override;
+  void setTimeout(std::chrono::milliseconds timeout) override { timeout_ = timeout; }
+  c10d::ErrorType getError() override;
+
   // ---- extras exposed to Python
   std::map<std::string, OpStats> stats();
   void reset_stats();

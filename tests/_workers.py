@@ -789,3 +789,34 @@ def autotune_fault_probe(rank, size, device="cuda"):
     dist.all_reduce(x)
     ok.append(bool(torch.all(x == size)))
     return {"ok": ok, "table": be.autotune_table()}
+
+
+def lifecycle_probe(rank, size, device="cpu"):
+    """c10d lifecycle hooks: aborting a sub-group (ProcessGroup.abort ->
+    Backend::abort) poisons it -- later calls fail fast with a clear error, getError
+    reports it -- while the default group keeps working; destroy_process_group on a
+    healthy group drains and shuts down cleanly."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    g = dist.new_group(list(range(size)))
+    t = torch.ones(4, device=d)
+    dist.all_reduce(t, group=g)
+    ok = {"before": bool(torch.all(t == size))}
+    g.abort()  # ProcessGroup.abort -> Backend::abort on every backend of the group
+    try:
+        dist.all_reduce(torch.ones(4, device=d), group=g)
+        ok["after_abort_raises"] = False
+    except RuntimeError as e:
+        ok["after_abort_raises"] = "error state" in str(e) or "aborted" in str(e)
+    t = torch.ones(4, device=d)
+    dist.all_reduce(t)
+    ok["default_group_alive"] = bool(torch.all(t == size))
+    h = dist.new_group(list(range(size)))
+    dist.all_reduce(t, group=h)
+    dist.destroy_process_group(h)
+    ok["healthy_flag"] = be.native_backend().healthy()
+    return ok

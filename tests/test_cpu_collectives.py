@@ -110,3 +110,8 @@ def test_p2p_between_two_ranks_of_a_larger_group(world):
     # send/recv must not need the other ranks of the group (pair channels)
     for ok in launch(W.p2p_subset, world, args=("cpu",), timeout_s=60, join_timeout_s=120):
         assert all(ok.values()), ok
+
+
+def test_abort_and_shutdown_hooks():
+    for ok in launch(W.lifecycle_probe, 2, args=("cpu",), timeout_s=60, join_timeout_s=120):
+        assert all(ok.values()), ok
