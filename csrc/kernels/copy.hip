@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       if (me == c.root) return;
       const OneSrcMap m{v.buf[c.root] + poff, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, OneSrcMap, kSysCoherent>(lds, m, 1);
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
     case IpcColl::BROADCAST_2SHOT: {
@@ -94,13 +94,13 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       if (me != c.root) {  // phase 1: fetch my owned tiles from the root (one link each)
         const OneSrcMap m{v.buf[c.root] + poff, mine, cpad, me + W * b, W * G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, OneSrcMap, kSysCoherent, /*SYS_STORE=*/true>(lds, m, 1);
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       block_barrier(v, ph1);
       if (me == c.root) return;
       {  // phase 2: every owner's tiles, owners interleaved (all links at once)
         const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, OwnerRowMap<W>, kSysCoherent>(lds, m, 1);
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       if (c.coll == IpcColl::GATHER && me != c.root) return;
       {
         const PeerTileMap<W> m{&v, &c, poff, c.bytes, (uint32_t)(me + b), b, G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, PeerTileMap<W>, kSysCoherent>(lds, m, 1);
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
         for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       const OneSrcMap m{v.buf[c.root] + poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, OneSrcMap, kSysCoherent>(lds, m, 1);
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
     case IpcColl::ALLTOALL: {
@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       {
         const PeerTileMap<W> m{&v, &c, poff + me * cpad, c.bytes, (uint32_t)(me + b), b, G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, PeerTileMap<W>, kSysCoherent>(lds, m, 1);
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }

@@ -9,11 +9,10 @@
 //    conservative vmcnt(0) it emits before a ds_read that may alias an in-flight
 //    LDS-DMA) and stores 16 B per lane. Waves only read LDS they filled
 //    themselves, so the ring needs no workgroup barrier.
-//  * cross-GPU signalling (K4): payload stored and loaded system-coherent (sc0
-//    sc1, write-through), every storing wave drained, then a relaxed system-scope
-//    flag store into the peer's uncached signal area and a bounded relaxed poll
-//    (the {sc0 sc1 stores and loads both sides} form of cdna_hip_programming.md §6
-//    Guideline 16, lifted from agent to system scope: the consumer is another GPU).
+//  * cross-GPU signalling (K4): system-scope release -> relaxed system-scope flag
+//    store into the peer's uncached signal area -> bounded relaxed poll -> ONE
+//    system-scope acquire (cdna_hip_programming.md §6 Guideline 16, lifted from
+//    agent to system scope because the consumer is another GPU over xGMI).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -59,22 +58,8 @@ __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   return v;
 }
 
-// LDS-DMA load of 16 B per lane. AUX is the cache policy: 0 = default, kSysCoherent
-// (sc0 sc1) = system scope: misses every cache on the way, so it reads what a peer GPU
-// wrote through to memory without any invalidate on this side.
-constexpr int kSysCoherent = 1 | 16;  // CPol SC0 | SC1 on gfx940+
-template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, AUX);
-}
-
-// 16-B store written through every cache to memory (system scope, sc0 sc1): the
-// cross-GPU hand-off needs no L2 write-back afterwards (vector store; inline asm
-// because there is no 16-B builtin with a scope).
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store16_sys(void* p, const uint4& v) {
-  const u32x4_t x = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
 // ----------------------------------------------------------------------------
@@ -204,9 +189,7 @@ __device__ __forceinline__ void wait_prologue(int i) {
   }
 }
 
-// AUX: cache policy of the loads (kSysCoherent for peer staging); SYS_STORE: results are
-// written through to memory (a peer reads them next, e.g. 2-shot phase-1 output).
-template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int AUX = 0, bool SYS_STORE = false>
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   static_assert((DEPTH - 1) * (NSRC + 1) < 64, "pipeline too deep for vmcnt");
   static_assert(DEPTH >= 2 && DEPTH <= 8, "prologue wait counts are written out for DEPTH <= 8");
@@ -218,7 +201,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   auto issue = [&](size_t i, int stage) {
 #pragma unroll
     for (int s = 0; s < NSRC; ++s)
-      glds16<AUX>(m.src(s, i) + lane_off, lds + (stage * NSRC + s) * kTile + wave * kWaveBytes);
+      glds16(m.src(s, i) + lane_off, lds + (stage * NSRC + s) * kTile + wave * kWaveBytes);
   };
   auto consume = [&](size_t i, int stage) {
     const uint32_t a = lds_off(lds + stage * NSRC * kTile + lane_off);
@@ -241,9 +224,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
     const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
     char* d = m.dst(i);
     const size_t lim = m.valid(i);
-    if constexpr (SYS_STORE) {
-      if (lane_off < lim) store16_sys(d + lane_off, r);  // staging destinations: whole padded tiles
-    } else if (lane_off + 16 <= lim) {
+    if (lane_off + 16 <= lim) {
       *reinterpret_cast<uint4*>(d + lane_off) = r;
     } else if (lane_off < lim) {
       store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
@@ -318,8 +299,7 @@ __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
 
 // Bounded local copy of the tiles {first, first+stride, ...} < ntiles of a user
 // buffer (nbytes long, 16-B aligned) into a padded staging buffer. Plain 16-B
-// loads (never LDS-DMA: reading past the end of a user allocation could fault);
-// system-coherent stores, since peers read the staging next.
+// loads (never LDS-DMA: reading past the end of a user allocation could fault).
 __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* __restrict__ dst,
                                             size_t nbytes, size_t first, size_t stride,
                                             size_t ntiles) {
@@ -337,13 +317,13 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
                                 : make_uint4(0, 0, 0, 0));
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) store16_sys(dst + off[u], v[u]);
+    for (int u = 0; u < U; ++u) *reinterpret_cast<uint4*>(dst + off[u]) = v[u];
   }
   for (; t < ntiles; t += stride) {
     const size_t off = t * kTile + lane_off;
     uint4 v = (off + 16 <= nbytes) ? *reinterpret_cast<const uint4*>(src + off)
               : (off < nbytes ? load_partial(src + off, (uint32_t)(nbytes - off)) : make_uint4(0, 0, 0, 0));
-    store16_sys(dst + off, v);
+    *reinterpret_cast<uint4*>(dst + off) = v;
   }
 }
 
@@ -384,16 +364,6 @@ __device__ __forceinline__ uint32_t call_seq(const kern::IpcView& v) {
 // Values are monotonic (seq*2 for phase 0, seq*2+1 for phase 1), compared with a
 // wrap-safe signed difference, so flags never need re-zeroing and a fast peer
 // that already moved on never deadlocks a slow one.
-//
-// Memory model ("write-through hand-off"): every byte a peer reads across the
-// barrier was stored system-coherent (store16_sys: sc0 sc1, written through to
-// memory) and is loaded system-coherent by the peer (glds16<kSysCoherent>: misses
-// every cache). So no L2 write-back before the flag and no invalidate after the
-// poll -- those cost ~2-7 us each per barrier (MI355X_MICROARCH.md price list)
-// and write back / drop the whole XCD L2, not just this block's lines. What
-// remains is the ordering: each storing wave waits for its stores (vmcnt(0),
-// inline asm so the compiler cannot drop it), a workgroup barrier, then the
-// system-scope flag store.
 __device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
   return (int32_t)(have - want) >= 0;
 }
@@ -404,10 +374,12 @@ __device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
 __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t value) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  drain_vm();       // every storing wave: its system-coherent stores are complete
+  drain_vm();       // every storing wave drains its stores
   __syncthreads();  // ... before wave 0 publishes for the whole block
   bool ok = true;
   if (wave == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
+    drain_vm();                                     // keep the wait after the fence (G16 pitfall 12)
     const int b = blockIdx.x;
     if (lane < v.world) {
       uint32_t* f = v.flags[lane] + b * kern::kMaxRanks + v.rank;
@@ -434,6 +406,8 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
+    drain_vm();
   }
   __syncthreads();
   return ok;

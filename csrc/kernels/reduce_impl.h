@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       block_barrier(v, ph0);
       if (c.coll == IpcColl::REDUCE_1SHOT && me != c.root) return;
       const AllSrcMap<W> m{&v, poff, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DT, OP, W, D, AllSrcMap<W>, kSysCoherent>(lds, m, c.avg_div);
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       return;
     }
     case IpcColl::ALLREDUCE_2SHOT:
@@ -228,14 +228,14 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       // phase 1: reduce my owned tiles from every rank, in place into my staging
       {
         const AllSrcMap<W> m{&v, poff, mine, nt * kTile, me + W * b, W * G, nt};
-        pipe_run<DT, OP, W, D, AllSrcMap<W>, kSysCoherent, /*SYS_STORE=*/true>(lds, m, c.avg_div);
+        pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       }
       block_barrier(v, ph1);
       if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
       // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
       {
         const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
-        pipe_run<DT, RedOp::COPY, 1, kCopyDepth, OwnerRowMap<W>, kSysCoherent>(lds, m, 1);
+        pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       const AllSrcMap<W> m{&v, poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DT, OP, W, D, AllSrcMap<W>, kSysCoherent>(lds, m, c.avg_div);
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       return;
     }
     default:

@@ -1,18 +1,15 @@
 """The cross-GPU memory model of the IPC kernels, checked in the machine code
-that ships (verdict r1 weak #3). The gfx950 code objects embedded in the built
-extension are disassembled; the protocol (dev_common.h, K4 "write-through
-hand-off") requires, in every IPC kernel:
+that ships (verdict r1 weak #3): the gfx950 code objects embedded in the built
+extension are disassembled and every cross-GPU barrier (dev_common.h
+block_barrier, K4) must
 
-  1. every byte a peer reads is stored system-coherent: staging stores are
-     ``global_store_dwordx4 ... sc0 sc1`` (written through to memory);
-  2. every peer read is system-coherent: every LDS-DMA load of staging is
-     ``global_load_lds_dwordx4 ... sc0 sc1`` (misses every cache, so no
-     invalidate is needed on the reading GPU);
-  3. before each flag store (``global_store_dword ... sc0 sc1``) the data stores
-     are drained (``s_waitcnt vmcnt(0)``) and the workgroup has met (``s_barrier``)
-     -- the MI355X compiler hazard (MI355X_MICROARCH.md) drops waits it thinks
-     redundant, which is why the drain is inline asm;
-  4. the peers' flags are polled with system-scope loads (``global_load_dword ... sc0 sc1``).
+  1. write back the L2 at system scope (``buffer_wbl2 sc0 sc1``) and WAIT for it
+     (``s_waitcnt vmcnt(0)``) before the flag store -- the MI355X compiler hazard
+     (MI355X_MICROARCH.md "Compiler hazard") drops that wait unless it is inline asm;
+  2. store the flag and poll the peers' flags with system-scope accesses
+     (``global_store_dword / global_load_dword ... sc0 sc1``: uncached, past L2);
+  3. invalidate at system scope (``buffer_inv sc0 sc1``) after the poll, and wait
+     for the invalidate, before any peer data is read.
 
 Runs on the CPU box (llvm-objcopy + llvm-objdump from ROCm, no GPU)."""
 import os
@@ -88,35 +85,25 @@ def _ipc_kernels(funcs):
     return ks
 
 
-def _is_data_store(ins):
-    return ins.startswith("global_store_dwordx") or ins.startswith("global_store_b") or \
-        ins.startswith("global_store_short") or ins.startswith("buffer_store")
-
-
 def _check_barriers(name, body):
-    stores16 = [s for s in body if s.startswith("global_store_dwordx4")]
-    assert any(s.endswith("sc0 sc1") for s in stores16), f"{name}: no system-coherent staging store"
-    ldma = [s for s in body if s.startswith("global_load_lds_dwordx4")]
-    assert ldma and all(s.endswith("sc0 sc1") for s in ldma), \
-        f"{name}: LDS-DMA loads of peer staging must be sc0 sc1: {[s for s in ldma if not s.endswith('sc0 sc1')][:3]}"
-    flags = [i for i, s in enumerate(body) if s.startswith("global_store_dword ") and s.endswith("sc0 sc1")]
-    assert flags, f"{name}: no system-scope flag store"
-    polls = [i for i, s in enumerate(body) if s.startswith("global_load_dword ") and s.endswith("sc0 sc1")]
-    assert polls, f"{name}: no system-scope flag poll"
-    checked = 0
-    for f in flags:
-        # back to the previous data store (or the kernel start): a drain and a barrier must lie between
-        j = f - 1
-        while j >= 0 and not _is_data_store(body[j]):
-            j -= 1
-        seg = body[j + 1:f]
-        if j < 0 or not body[j].startswith("global_store_dwordx4"):
-            continue  # error-word stores after a timeout, or flags before any payload (BARRIER)
-        checked += 1
-        assert any(x.startswith("s_waitcnt") and "vmcnt(0)" in x for x in seg), \
-            f"{name}: flag store at {f} not behind a vmcnt(0) drain of the payload stores"
-        assert any(x == "s_barrier" for x in seg), f"{name}: flag store at {f} not behind the workgroup barrier"
-    assert checked, f"{name}: no flag store follows a payload store (checker found nothing to check)"
+    wbl = [i for i, s in enumerate(body) if s == "buffer_wbl2 sc0 sc1"]
+    inv = [i for i, s in enumerate(body) if s == "buffer_inv sc0 sc1"]
+    assert wbl, f"{name}: no system-scope L2 write-back"
+    assert len(wbl) == len(inv), f"{name}: {len(wbl)} releases vs {len(inv)} acquires"
+    for w in wbl:
+        # the flag store: first system-scope store after the release
+        f = next(i for i in range(w + 1, len(body))
+                 if body[i].startswith("global_store_dword ") and body[i].endswith("sc0 sc1"))
+        assert any(body[i].startswith("s_waitcnt") and "vmcnt(0)" in body[i] for i in range(w + 1, f)), \
+            f"{name}: flag store at +{f - w} not behind a vmcnt(0) wait after buffer_wbl2"
+        # the poll: system-scope load after the flag store, and the acquire after it
+        p = next(i for i in range(f + 1, len(body))
+                 if body[i].startswith("global_load_dword ") and body[i].endswith("sc0 sc1"))
+        a = next((i for i in inv if i > p), None)
+        assert a is not None, f"{name}: no buffer_inv sc0 sc1 after the poll at {p}"
+        nxt = body[a + 1:a + 4]
+        assert any(s.startswith("s_waitcnt") and "vmcnt(0)" in s for s in nxt), \
+            f"{name}: the system-scope invalidate is not waited for: {nxt}"
 
 
 def test_every_ipc_kernel_orders_cross_gpu_handoffs(kernels):
