@@ -618,6 +618,13 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
 
 void ProcessGroupMI355X::abort() { abort_group("aborted by ProcessGroup.abort()"); }
 
+std::vector<std::vector<uint64_t>> ProcessGroupMI355X::ipc_trace() {
+  std::lock_guard<std::mutex> lk(init_mu_);
+  for (auto& kv : devs_)
+    if (kv.second->ipc) return kv.second->ipc->trace_records();
+  return {};
+}
+
 // Orderly shutdown (destroy_process_group): let enqueued GPU work drain for up to the
 // group timeout; a group that cannot drain (a peer is gone) is aborted instead of hanging.
 void ProcessGroupMI355X::shutdown() {

@@ -281,6 +281,8 @@ class ProcessGroupMI355X : public c10d::Backend {
   void abort_group(const std::string& why);
   // set up device state, topology and the RCCL communicator now (PDCC_EAGER_INIT)
   void eager_init(int device);
+  // PDCC_IPC_TRACE records of this group's IPC kernels (block 0 phase timestamps)
+  std::vector<std::vector<uint64_t>> ipc_trace();
   // runtime overrides (must be applied identically on every rank of the group)
   void set_algo(const std::string& a);
   void set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max);

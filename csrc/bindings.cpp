@@ -155,6 +155,9 @@ PYBIND11_MODULE(_C, m) {
       .def("set_ipc_thresholds", &pdcc::ProcessGroupMI355X::set_ipc_thresholds, py::arg("one_shot_max") = -1,
            py::arg("two_shot_max") = -1, py::arg("copy_max") = -1)
       .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>())
+      .def("ipc_trace", &pdcc::ProcessGroupMI355X::ipc_trace,
+           "PDCC_IPC_TRACE records: [seq, t_entry, t_seq, t_staged, t_barrier0, t_phase1, t_barrier1, t_exit] "
+           "in 100 MHz device ticks, block 0 of each IPC kernel")
       .def("eager_init", &pdcc::ProcessGroupMI355X::eager_init, py::arg("device"),
            py::call_guard<py::gil_scoped_release>());
 

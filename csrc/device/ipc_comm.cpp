@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 
@@ -120,6 +121,16 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
     *err_host_ = 0;
     PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
+    if (const char* tr = std::getenv("PDCC_IPC_TRACE")) {
+      const long n = std::atol(tr);
+      if (n > 0) {
+        trace_cap_ = (uint32_t)std::min<long>(n, 1 << 20);
+        const size_t tb = (size_t)trace_cap_ * kern::kTraceWords * sizeof(uint64_t);
+        PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&trace_host_), tb, hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(trace_host_, 0, tb);
+        PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&trace_dev_), trace_host_, 0));
+      }
+    }
     PDCC_HIP(hipDeviceSynchronize());
   } catch (const std::exception& e) {
     err = e.what();
@@ -156,6 +167,7 @@ IpcComm::~IpcComm() {
       if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
     if (err_host_) hipHostFree(err_host_);
+    if (trace_host_) hipHostFree(trace_host_);
   } catch (...) {
   }
 }
@@ -256,6 +268,8 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   v.seq = seq_;
   v.dev_seq = graph_mode_ ? 1u : 0u;
   v.timeout_ticks = timeout_ticks_;
+  v.trace = trace_dev_;
+  v.trace_cap = trace_cap_;
   if (shared_device_) {
     // all ranks' grids must be co-resident on ONE device (test setups): stay well
     // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
@@ -269,6 +283,17 @@ uint32_t IpcComm::error_word() const { return err_host_ ? __atomic_load_n(err_ho
 void IpcComm::clear_error() {
   if (err_host_) __atomic_store_n(err_host_, 0u, __ATOMIC_RELEASE);
 }
+std::vector<std::vector<uint64_t>> IpcComm::trace_records() const {
+  std::vector<std::vector<uint64_t>> out;
+  for (uint32_t i = 0; trace_host_ && i < trace_cap_; ++i) {
+    const volatile uint64_t* r = trace_host_ + (size_t)i * kern::kTraceWords;
+    if (r[1] == 0) continue;  // never written
+    out.emplace_back(r, r + kern::kTraceWords);
+  }
+  std::sort(out.begin(), out.end(), [](const auto& a, const auto& b) { return a[1] < b[1]; });
+  return out;
+}
+
 void IpcComm::abort() {
   if (!err_host_) return;
   uint32_t expect = 0;

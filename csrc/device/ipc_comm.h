@@ -55,6 +55,10 @@ class IpcComm {
   // kernels spinning in a cross-GPU barrier see it within ~256 polls and leave.
   static constexpr uint32_t kAbortWord = 0x200u;
   void abort();
+
+  // PDCC_IPC_TRACE=N: kernels record per-phase device timestamps of block 0 into a
+  // host-mapped ring of N records (kern::kTraceWords u64 each); copies of the valid ones
+  std::vector<std::vector<uint64_t>> trace_records() const;
   bool shared_device() const { return shared_device_; }
   int world() const { return world_; }
   uint64_t calls() const { return seq_; }
@@ -75,6 +79,9 @@ class IpcComm {
   std::vector<void*> flags_maps_;         // hipIpcOpenMemHandle results to close (may precede the pointer)
   uint32_t* err_host_ = nullptr;          // pinned, device-visible
   uint32_t* err_dev_ = nullptr;
+  uint64_t* trace_host_ = nullptr;        // PDCC_IPC_TRACE ring (pinned, device-visible), or null
+  uint64_t* trace_dev_ = nullptr;
+  uint32_t trace_cap_ = 0;
 
   char* my_staging_ = nullptr;
   size_t cap_ = 0;                         // bytes per parity

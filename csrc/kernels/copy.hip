@@ -68,7 +68,10 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
+  PhaseTrace tr(v);
   const uint32_t seq = call_seq(v);
+  tr.t[0] = seq;
+  tr.mark(2);
   const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
   const size_t poff = (seq & 1u) ? v.cap : 0;
   char* mine = v.buf[me] + poff;
@@ -81,7 +84,9 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
       return;
     case IpcColl::BROADCAST_1SHOT: {
       if (me == c.root) stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      tr.mark(3);
       block_barrier(v, ph0);
+      tr.mark(4);
       if (me == c.root) return;
       const OneSrcMap m{v.buf[c.root] + poff, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
@@ -107,7 +112,9 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
     case IpcColl::ALLGATHER:
     case IpcColl::GATHER: {
       stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      tr.mark(3);
       block_barrier(v, ph0);
+      tr.mark(4);
       if (c.coll == IpcColl::GATHER && me != c.root) return;
       {
         const PeerTileMap<W> m{&v, &c, poff, c.bytes, (uint32_t)(me + b), b, G, nt};

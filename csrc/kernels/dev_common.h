@@ -358,6 +358,32 @@ __device__ __forceinline__ uint32_t call_seq(const kern::IpcView& v) {
 }
 
 // ----------------------------------------------------------------------------
+// Phase trace (PDCC_IPC_TRACE): block 0 / thread 0 keeps timestamps in registers
+// and writes the record once, when the kernel returns (no extra memory traffic
+// inside the protocol).
+struct PhaseTrace {
+  const kern::IpcView& v;
+  uint64_t t[kern::kTraceWords];
+  bool on;
+  __device__ explicit PhaseTrace(const kern::IpcView& view)
+      : v(view), on(view.trace != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < kern::kTraceWords; ++k) t[k] = 0;
+    if (on) t[1] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if (on) t[k] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ ~PhaseTrace() {
+    if (!on) return;
+    t[7] = __builtin_amdgcn_s_memrealtime();
+    uint64_t* r = v.trace + (size_t)(t[0] % v.trace_cap) * kern::kTraceWords;
+#pragma unroll
+    for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];
+  }
+};
+
+// ----------------------------------------------------------------------------
 // K4: cross-GPU block-pairwise barrier.
 //
 // flags layout (per rank, uncached device memory): flags[block * kMaxRanks + src].

@@ -91,7 +91,15 @@ struct IpcView {
   uint32_t seq;                // host-issued call sequence number, identical on every rank
   uint32_t dev_seq;            // 1: graph-captured launch, take the number from seq_dev
   uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
+  uint64_t* trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
+  uint32_t trace_cap;          // records in the ring
 };
+
+// Device-side phase trace of an IPC call (block 0, s_memrealtime ticks at 100 MHz):
+// [0] call sequence number, [1] entry, [2] sequence number known, [3] local data
+// staged, [4] first cross-GPU barrier passed, [5] first pull / reduce done,
+// [6] second barrier passed (2-shot), [7] exit. Record `seq % trace_cap`.
+constexpr int kTraceWords = 8;
 
 enum class IpcColl : int32_t {
   ALLREDUCE_1SHOT = 0,   // stage, barrier, every rank reduces everything from all peers

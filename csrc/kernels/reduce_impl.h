@@ -204,7 +204,10 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, D>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
+  PhaseTrace tr(v);
   const uint32_t seq = call_seq(v);
+  tr.t[0] = seq;
+  tr.mark(2);
   const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
   const size_t poff = (seq & 1u) ? v.cap : 0;
   char* mine = v.buf[me] + poff;
@@ -214,23 +217,30 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
     case IpcColl::ALLREDUCE_1SHOT:
     case IpcColl::REDUCE_1SHOT: {
       stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
+      tr.mark(3);
       block_barrier(v, ph0);
+      tr.mark(4);
       if (c.coll == IpcColl::REDUCE_1SHOT && me != c.root) return;
       const AllSrcMap<W> m{&v, poff, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      tr.mark(5);
       return;
     }
     case IpcColl::ALLREDUCE_2SHOT:
     case IpcColl::REDUCE_2SHOT: {
       // stage the rows of this block: tiles q + W*(b + G*k) for every owner q
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[0], mine, c.bytes, q + W * b, W * G, nt);
+      tr.mark(3);
       block_barrier(v, ph0);
+      tr.mark(4);
       // phase 1: reduce my owned tiles from every rank, in place into my staging
       {
         const AllSrcMap<W> m{&v, poff, mine, nt * kTile, me + W * b, W * G, nt};
         pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
       }
+      tr.mark(5);
       block_barrier(v, ph1);
+      tr.mark(6);
       if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
       // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
       {
@@ -242,9 +252,12 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
     case IpcColl::REDUCE_SCATTER: {
       const size_t cpad = pad_tiles(c.bytes);
       for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
+      tr.mark(3);
       block_barrier(v, ph0);
+      tr.mark(4);
       const AllSrcMap<W> m{&v, poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
       pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      tr.mark(5);
       return;
     }
     default:
