@@ -17,7 +17,7 @@ struct Config {
   size_t ipc_1shot_max = 512u << 10;       // PDCC_IPC_1SHOT_MAX   all-reduce/reduce <= this: 1-shot
   size_t ipc_2shot_max = 8u << 20;         // PDCC_IPC_2SHOT_MAX   <= this: 2-shot, else RCCL
   size_t ipc_copy_max = 1u << 20;          // PDCC_IPC_COPY_MAX    broadcast/gather/... <= this: IPC
-  size_t ipc_max_staging = 512u << 20;     // PDCC_IPC_MAX_STAGING per parity; larger messages are chunked
+  size_t ipc_max_staging = 1u << 30;       // PDCC_IPC_MAX_STAGING staging bytes; larger messages are chunked
   bool ipc_enable = true;                  // PDCC_IPC=0 disables the peer-memory path
   // Before a group first uses a device, every rank runs the IPC protocol once on known data (1-shot
   // and 2-shot all-reduce, all-gather) with a short spin timeout and checks the results; one failure

@@ -194,7 +194,7 @@ void IpcComm::map_staging(size_t cap) {
   std::string err;
   char* fresh = nullptr;
   try {
-    fresh = static_cast<char*>(alloc_exportable(granule(2 * cap), false, mine));
+    fresh = static_cast<char*>(alloc_exportable(granule(cap), false, mine));
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();
@@ -251,22 +251,20 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
           "(parallel.graphs.capture does)");
     ensure_staging(need, stream);
   }
-  // Once a launch is captured, sequence numbers live on the device for good: a
-  // graph replays its kernel arguments verbatim, so the host count would go stale.
+  // A captured graph bakes the staging pointers into its kernel arguments: from
+  // now on staging is retired, never freed, when it grows.
   if (capturing) graph_mode_ = true;
   kern::IpcView v{};
-  ++seq_;  // flags compare with a wrap-safe signed difference, so uint32 wrap is harmless
+  ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
   for (int r = 0; r < world_; ++r) {
-    v.buf[r] = peer_staging_.empty() ? nullptr : peer_staging_[r];  // parity 0; the kernel adds cap for parity 1
+    v.buf[r] = peer_staging_.empty() ? nullptr : peer_staging_[r];
     v.flags[r] = peer_flags_[r];
   }
   v.err = err_dev_;
-  v.seq_dev = my_flags_;
+  v.counters = my_flags_ + kern::kCountWord;
   v.cap = cap_;
   v.rank = rank_;
   v.world = world_;
-  v.seq = seq_;
-  v.dev_seq = graph_mode_ ? 1u : 0u;
   v.timeout_ticks = timeout_ticks_;
   v.trace = trace_dev_;
   v.trace_cap = trace_cap_;

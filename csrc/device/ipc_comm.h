@@ -1,18 +1,21 @@
 // Peer-memory (hipIpc over xGMI) communicator: every rank owns
-//   * a staging buffer of 2 parities x `cap` bytes (coarse-grained HBM), and
-//   * a signal area (uncached device memory) holding the block-pairwise flags,
+//   * a staging buffer of `cap` bytes (coarse-grained HBM), and
+//   * a signal area (uncached device memory) holding the block-pairwise flags
+//     and the per-block call counters,
 // and maps every peer's staging + signal area into its own address space. The
 // IPC collective kernels (csrc/kernels) stage local data into the own buffer,
 // flag the peers, and pull/reduce straight out of the peers' buffers -- all 7
 // xGMI links of a node busy at once instead of one ring neighbour.
 //
-// Consecutive calls alternate parity, which makes an end-of-call barrier
-// unnecessary: before a rank writes a parity again, the start barrier of the
-// call in between proves every peer has finished the call that last read it.
+// Every call starts with an arrival barrier (block b waits until block b of
+// every peer has started the same call): since kernels on a stream run in order,
+// that proves every peer's previous call has finished reading the staging this
+// call is about to overwrite, whatever grids the two calls had. One staging
+// buffer suffices, and no host-side sequence number is involved.
 //
-// Launches may be captured into a hipGraph (parallel/graphs.py): from the first
-// captured launch on, the kernels take their sequence number from a counter in
-// the own signal area, and staging a graph may reference is retired, not freed.
+// Launches may be captured into a hipGraph (parallel/graphs.py) and replayed
+// freely (the kernels' per-block counters live on the device); staging a graph
+// may reference is retired, not freed, when it grows.
 #pragma once
 #include <hip/hip_runtime_api.h>
 #include <torch/csrc/distributed/c10d/Store.hpp>
@@ -84,7 +87,7 @@ class IpcComm {
   uint32_t trace_cap_ = 0;
 
   char* my_staging_ = nullptr;
-  size_t cap_ = 0;                         // bytes per parity
+  size_t cap_ = 0;                         // staging bytes
   std::vector<char*> peer_staging_;
   std::vector<void*> staging_maps_;
   int staging_gen_ = 0;

@@ -64,24 +64,24 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 
 // ----------------------------------------------------------- IPC copy family
 template <int W>
-__global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
-  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+__device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  PhaseTrace tr(v);
-  const uint32_t seq = call_seq(v);
-  tr.t[0] = seq;
+  const uint32_t seq = block_seq(v);
+  tr.seq(seq);
+  const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
+  if (c.coll == IpcColl::BARRIER) {  // the arrival barrier is the whole collective
+    block_barrier<false>(v, ep);
+    return;
+  }
+  block_barrier<false>(v, ep);  // arrival: every peer's previous call is over
   tr.mark(2);
-  const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
-  const size_t poff = (seq & 1u) ? v.cap : 0;
-  char* mine = v.buf[me] + poff;
+  const size_t poff = 0;        // single staging buffer (the arrival barrier guards reuse)
+  char* mine = v.buf[me];
   const size_t nt = pad_tiles(c.bytes) / kTile;
   const size_t cpad = nt * kTile;
 
   switch (c.coll) {
-    case IpcColl::BARRIER:
-      block_barrier(v, ph0);
-      return;
     case IpcColl::BROADCAST_1SHOT: {
       if (me == c.root) stage_tiles((const char*)c.in[0], mine, c.bytes, b, G, nt);
       tr.mark(3);
@@ -142,6 +142,14 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
     default:
       return;
   }
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+  PhaseTrace tr(v);
+  ipc_copy_body<W>(v, c, lds, tr);
+  tr.finish(v);
 }
 
 }  // namespace dev
@@ -248,8 +256,8 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
   return hipSuccess;
 }
 
-// block-pairwise flags, then the sequence counter (kSeqWord) and arrivals (kArriveWord)
-size_t ipc_signal_bytes() { return (size_t)(kArriveWord + 16) * sizeof(uint32_t); }
+// block-pairwise flags, then the per-block call counters
+size_t ipc_signal_bytes() { return (size_t)(kCountWord + kMaxBlocks) * sizeof(uint32_t); }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;

@@ -328,29 +328,17 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
 }
 
 // ----------------------------------------------------------------------------
-// Sequence number of this IPC call (see kern::IpcView). Host-issued launches
-// pass it in the view and block 0 records it in the device counter. Graph-
-// captured launches read counter + 1 in every block; each block then arrives on
-// a counter with a release-ordered RMW (after its read), and the last arriver
-// resets the arrivals and publishes the new number for the next launch, so no
-// block can see it early. Uncached signal memory: no stale L2 line on any XCD.
-__device__ __forceinline__ uint32_t call_seq(const kern::IpcView& v) {
+// This block's call number (see kern::IpcView): thread 0 reads its own counter
+// and writes it back incremented. Only block b of this rank ever touches
+// counters[b], and consecutive launches on a stream run in order, so relaxed
+// accesses suffice (uncached signal memory: no stale line on any XCD); the store
+// is drained by the arrival barrier that follows.
+__device__ __forceinline__ uint32_t block_seq(const kern::IpcView& v) {
   __shared__ uint32_t s_seq;
   if (threadIdx.x == 0) {
-    uint32_t s;
-    uint32_t* const word = v.seq_dev + kern::kSeqWord;
-    if (v.dev_seq) {
-      uint32_t* const arrive = v.seq_dev + kern::kArriveWord;
-      s = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-      const uint32_t n = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (n == gridDim.x - 1) {
-        __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(word, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      s = v.seq;
-      if (blockIdx.x == 0) __hip_atomic_store(word, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    uint32_t* const c = v.counters + blockIdx.x;
+    const uint32_t s = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq = s;
   }
   __syncthreads();
@@ -359,25 +347,35 @@ __device__ __forceinline__ uint32_t call_seq(const kern::IpcView& v) {
 
 // ----------------------------------------------------------------------------
 // Phase trace (PDCC_IPC_TRACE): block 0 / thread 0 keeps timestamps in registers
-// and writes the record once, when the kernel returns (no extra memory traffic
-// inside the protocol).
+// and writes the record once, when the kernel body returns (finish(); no extra
+// memory traffic inside the protocol).
+// The record lives in LDS (64 B per workgroup): a trace object in registers gets
+// demoted to scratch memory once it crosses the kernel body's many exit paths.
 struct PhaseTrace {
-  const kern::IpcView& v;
-  uint64_t t[kern::kTraceWords];
-  bool on;
-  __device__ explicit PhaseTrace(const kern::IpcView& view)
-      : v(view), on(view.trace != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+  const bool on;
+  __device__ __forceinline__ static uint64_t* slots() {
+    __shared__ uint64_t s[kern::kTraceWords];
+    return s;
+  }
+  __device__ __forceinline__ explicit PhaseTrace(const kern::IpcView& view)
+      : on(view.trace != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (on) {
 #pragma unroll
-    for (int k = 0; k < kern::kTraceWords; ++k) t[k] = 0;
-    if (on) t[1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = 0; k < kern::kTraceWords; ++k) slots()[k] = 0;
+      slots()[1] = __builtin_amdgcn_s_memrealtime();
+    }
   }
-  __device__ __forceinline__ void mark(int k) {
-    if (on) t[k] = __builtin_amdgcn_s_memrealtime();
+  __device__ __forceinline__ void seq(uint32_t s) const {
+    if (on) slots()[0] = s;
   }
-  __device__ ~PhaseTrace() {
+  __device__ __forceinline__ void mark(int k) const {
+    if (on) slots()[k] = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ void finish(const kern::IpcView& view) const {
     if (!on) return;
+    uint64_t* t = slots();
     t[7] = __builtin_amdgcn_s_memrealtime();
-    uint64_t* r = v.trace + (size_t)(t[0] % v.trace_cap) * kern::kTraceWords;
+    uint64_t* r = view.trace + (size_t)(t[0] % view.trace_cap) * kern::kTraceWords;
 #pragma unroll
     for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];
   }
@@ -387,16 +385,22 @@ struct PhaseTrace {
 // K4: cross-GPU block-pairwise barrier.
 //
 // flags layout (per rank, uncached device memory): flags[block * kMaxRanks + src].
-// Values are monotonic (seq*2 for phase 0, seq*2+1 for phase 1), compared with a
-// wrap-safe signed difference, so flags never need re-zeroing and a fast peer
-// that already moved on never deadlocks a slow one.
+// Values are monotonic epochs (kEpochsPerCall * seq + phase, seq = the block's
+// call number), compared with a wrap-safe signed difference, so flags never need
+// re-zeroing and a fast peer that already moved on never deadlocks a slow one.
 __device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
   return (int32_t)(have - want) >= 0;
 }
 
 // Every wave of the block calls this after its last store of data that peers
-// will read. Returns false on timeout (error word set, block continues so the
-// grid always drains).
+// will read (DATA = true: system-scope release before the flag, acquire after the
+// poll). DATA = false is the arrival barrier at the start of a call: nothing is
+// handed over, so no cache maintenance -- it only proves that every peer's block
+// of the same index has started this call, i.e. (same-stream kernels run in
+// order) that every peer's previous kernel has finished and no longer reads the
+// staging this call is about to overwrite. Returns false on timeout (error word
+// set, block continues so the grid always drains).
+template <bool DATA = true>
 __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t value) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -404,8 +408,10 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
   __syncthreads();  // ... before wave 0 publishes for the whole block
   bool ok = true;
   if (wave == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
-    drain_vm();                                     // keep the wait after the fence (G16 pitfall 12)
+    if constexpr (DATA) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
+      drain_vm();                                     // keep the wait after the fence (G16 pitfall 12)
+    }
     const int b = blockIdx.x;
     if (lane < v.world) {
       uint32_t* f = v.flags[lane] + b * kern::kMaxRanks + v.rank;
@@ -432,8 +438,10 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
-    drain_vm();
+    if constexpr (DATA) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
+      drain_vm();
+    }
   }
   __syncthreads();
   return ok;

@@ -71,34 +71,31 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 // ---------------------------------------------------------------- IPC collectives
 // Per-rank view of the group's registered (hipIpc) memory for ONE call.
 //
-// The call's sequence number picks the staging parity (seq & 1) and the flag
-// epochs (2 seq, 2 seq + 1). Host-issued launches carry it in `seq`. A hipGraph
-// replays kernel arguments verbatim, so launches captured into a graph set
-// `dev_seq` and every block derives the number from the rank's own device
-// counter instead (seq_dev[kSeqWord] + 1; the last block to arrive publishes
-// it). Host-issued launches keep that counter current, so a group can switch
-// to graph mode at any call.
-constexpr int kSeqWord = kMaxBlocks * kMaxRanks;  // u32 index of the counter in the signal area
-constexpr int kArriveWord = kSeqWord + 16;        // arrivals of the current graph-mode launch
+// Sequencing is per workgroup and lives on the device: block b of every rank
+// keeps a call counter in its own signal area (counters[b]), bumps it at entry
+// and derives its flag epochs from it. Block b takes part in the same calls on
+// every rank (the grid is a function of the call's arguments only), so the
+// counters agree without any host-side number -- eager launches and graph
+// replays (which repeat kernel arguments verbatim) run the same code.
+constexpr int kCountWord = kMaxBlocks * kMaxRanks;  // u32 index of counters[0] in the signal area
+constexpr int kEpochsPerCall = 4;                   // arrival, data, second data phase (+1 spare)
 struct IpcView {
-  char* buf[kMaxRanks];        // staging buffer (parity 0; parity 1 starts at + cap), per rank (own included)
+  char* buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes
   uint32_t* flags[kMaxRanks];  // signal area (uncached device memory) per rank
   uint32_t* err;               // host-mapped error word (0 = ok), written on spin timeout
-  uint32_t* seq_dev;           // own signal area (sequence counter at kSeqWord, arrivals at kArriveWord)
-  size_t cap;                  // bytes per staging parity
+  uint32_t* counters;          // own signal area + kCountWord: per-block call counters
+  size_t cap;                  // staging bytes
   int rank;
   int world;
-  uint32_t seq;                // host-issued call sequence number, identical on every rank
-  uint32_t dev_seq;            // 1: graph-captured launch, take the number from seq_dev
   uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
   uint64_t* trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
   uint32_t trace_cap;          // records in the ring
 };
 
 // Device-side phase trace of an IPC call (block 0, s_memrealtime ticks at 100 MHz):
-// [0] call sequence number, [1] entry, [2] sequence number known, [3] local data
-// staged, [4] first cross-GPU barrier passed, [5] first pull / reduce done,
-// [6] second barrier passed (2-shot), [7] exit. Record `seq % trace_cap`.
+// [0] block 0's call number, [1] entry, [2] arrival barrier passed, [3] local data
+// staged, [4] data barrier passed, [5] first pull / reduce done, [6] second data
+// barrier passed (2-shot), [7] exit. Record `seq % trace_cap`.
 constexpr int kTraceWords = 8;
 
 enum class IpcColl : int32_t {
@@ -132,7 +129,7 @@ struct IpcCall {
   void* out[kMaxRanks];          // local outputs: out[0] single, out[c] per chunk for lists
 };
 
-// Bytes of staging needed per parity for `call` (padded to tiles).
+// Bytes of staging needed for `call` (padded to tiles).
 size_t ipc_staging_bytes(const IpcCall& call, int world);
 // Bytes of the signal area every rank must allocate (uncached memory).
 size_t ipc_signal_bytes();

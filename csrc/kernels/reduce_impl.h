@@ -138,7 +138,7 @@ constexpr int kCopyDepth = 4;
 template <int W>
 struct OwnerRowMap {
   const IpcView* v;
-  size_t poff;  // staging parity offset of this call
+  size_t poff;  // offset of this call in the staging buffers (0: one buffer)
   char* d;
   size_t dlim;
   uint32_t rot;
@@ -171,7 +171,7 @@ template <int W>
 struct PeerTileMap {
   const IpcView* v;
   const IpcCall* c;
-  size_t sbase;  // parity offset + chunk offset inside each staging buffer
+  size_t sbase;  // offset of the chunk inside each staging buffer
   size_t dlim;
   uint32_t rot;
   size_t first, stride, ntiles;
@@ -199,18 +199,17 @@ struct PeerTileMap {
 };
 
 template <DType DT, RedOp OP, int W>
-__global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
+__device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
   constexpr int D = DepthFor<W>::value;
-  __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, D>::kBytes];
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  PhaseTrace tr(v);
-  const uint32_t seq = call_seq(v);
-  tr.t[0] = seq;
+  const uint32_t seq = block_seq(v);
+  tr.seq(seq);
+  const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
+  block_barrier<false>(v, ep);  // arrival: every peer's previous call is over
   tr.mark(2);
-  const uint32_t ph0 = seq * 2u, ph1 = seq * 2u + 1u;
-  const size_t poff = (seq & 1u) ? v.cap : 0;
-  char* mine = v.buf[me] + poff;
+  const size_t poff = 0;        // single staging buffer (the arrival barrier guards reuse)
+  char* mine = v.buf[me];
   const size_t nt = pad_tiles(c.bytes) / kTile;
 
   switch (c.coll) {
@@ -263,6 +262,14 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
     default:
       return;
   }
+}
+
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
+  __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, DepthFor<W>::value>::kBytes];
+  PhaseTrace tr(v);
+  ipc_reduce_body<DT, OP, W>(v, c, lds, tr);
+  tr.finish(v);
 }
 
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)

@@ -14,7 +14,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_1SHOT_MAX | 512K | all-reduce/reduce/broadcast up to this size: 1-shot protocol |
 | PDCC_IPC_2SHOT_MAX | 8M | ... up to this size: 2-shot; above: RCCL |
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
-| PDCC_IPC_MAX_STAGING | 512M | staging bytes per parity; larger calls are chunked |
+| PDCC_IPC_MAX_STAGING | 1G | staging bytes; larger calls are chunked |
 | PDCC_IPC_SPIN_MS | 600000 | bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if shorter) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
@@ -71,7 +71,7 @@ class Config:
     ipc_1shot_max: int = 512 << 10
     ipc_2shot_max: int = 8 << 20
     ipc_copy_max: int = 1 << 20
-    ipc_max_staging: int = 512 << 20
+    ipc_max_staging: int = 1 << 30
     ipc_spin_ms: int = 600000
     autotune: bool = True
     autotune_min: int = 64 << 10

@@ -10,10 +10,10 @@ What the backend does while the caller's stream is being captured
 
 * every collective is enqueued on the capturing stream and returns an
   already-completed Work -- the graph node is the completion;
-* the IPC kernels take their call sequence number from a per-rank device
-  counter instead of a kernel argument (a graph replays arguments verbatim), so
-  flag epochs and staging parities advance on every replay exactly as for eager
-  calls, and eager calls can be interleaved with replays;
+* the IPC kernels keep their call numbers on the device (per-block counters,
+  csrc/kernels/kernel_api.h), never in a kernel argument (a graph replays
+  arguments verbatim), so flag epochs advance on every replay exactly as for
+  eager calls, and eager calls can be interleaved with replays;
 * RCCL calls are captured as RCCL graph nodes;
 * staging buffers a captured graph references are never freed while the group
   lives (a later, larger call grows into new buffers instead);

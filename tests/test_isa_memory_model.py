@@ -117,3 +117,14 @@ def test_lds_dma_engine_in_the_shipped_kernels(kernels):
     assert names
     for n in names:
         assert any(s.startswith("global_load_lds_dwordx4") for s in kernels[n]), n
+
+
+def test_no_scratch_in_the_hot_kernels(kernels):
+    # a register spill, a private copy of the kernel-argument view (e.g. a reference to it kept in a
+    # struct) or an out-of-line device call puts state in scratch and turns peer pointers into flat
+    # ones -- check it never ships
+    names = [n for n in kernels if "k1_reduce" in n or "k2_multi_copy" in n or "k_ipc_" in n]
+    assert names
+    for n in names:
+        bad = [s for s in kernels[n] if s.startswith(("scratch_", "flat_", "s_swappc"))]  # spills, flat, calls
+        assert not bad, (n, bad[:4])
