@@ -458,7 +458,10 @@ def rccl_tuning(world, rank, dev, x):
 
 def graph_replay(world, rank, dev, n_ops=16, numel=1024):
     """hipGraph replay vs eager issue of a launch-bound step: n_ops small
-    all_reduces captured with parallel.graphs.capture, checked afterwards."""
+    all_reduces captured with parallel.graphs.capture, checked afterwards.
+    (With ranks sharing one GPU -- rehearsals only -- the processes' hardware
+    queues get time-sliced after the capture and replays look slow; see
+    scripts/graph_bench.py. One process per GPU is not affected.)"""
     import torch
     import torch.distributed as dist
 

@@ -37,6 +37,7 @@ for s in "$@"; do
     churn) step churn 300 python scripts/group_churn.py ;;
     graphprobe) step graphprobe 300 python scripts/graph_probe.py ;;
     graphrt) step graphrt 200 python scripts/graph_rt_probe.py ;;
+    graphprobe_q1) GPU_MAX_HW_QUEUES=1 step graphprobe_q1 300 python scripts/graph_probe.py ;;
     graphprof) step graphprof 400 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$0/gpurun_out/prof_graph" -o g -- python3 "$0/scripts/graph_bench.py"' "$(pwd)" ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \

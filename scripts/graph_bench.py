@@ -6,7 +6,14 @@ all_reduces (4 KiB each), captured with parallel.graphs.capture.
     GRAPH_BENCH_MODE=rccl1 python scripts/graph_bench.py   # 1 rank, RCCL forced (PDCC_WORLD1_LOCAL=0)
 
 On one GPU the IPC "peers" are local HBM, so this measures the host launch and
-protocol cost per step -- exactly what a graph replay removes. Prints one JSON line.
+protocol cost per step -- exactly what a graph replay removes. The two ranks
+share the GPU, so each process is held to one hardware queue
+(GPU_MAX_HW_QUEUES=1): the capture's side stream would otherwise give each
+process more queues than the GPU maps at once, and the hardware scheduler then
+time-slices the two processes' queues -- the IPC kernels of one rank wait a
+slice (~40 us) for the peer's (profiles/graph_probe_r2.jsonl vs
+graph_probe_q1_r2.jsonl). One process per GPU never shares a GPU's queues.
+Prints one JSON line.
 """
 import json
 import os
@@ -61,7 +68,8 @@ if __name__ == "__main__":
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     mode = os.environ.get("GRAPH_BENCH_MODE", "ipc2")
-    world, env = (1, {"PDCC_WORLD1_LOCAL": "0"}) if mode == "rccl1" else (2, {"PDCC_ALGO": "ipc"})
+    world, env = (1, {"PDCC_WORLD1_LOCAL": "0"}) if mode == "rccl1" else (2, {"PDCC_ALGO": "ipc",
+                                                                          "GPU_MAX_HW_QUEUES": "1"})
     out = launch(work, world, args=(16, 1024, 50), bind_device=True, timeout_s=60, env=env, join_timeout_s=300)
     print(json.dumps({"mode": mode, "ranks_on_one_gpu": world, "ops_per_step": 16, "bytes_per_op": 4096,
                       "per_rank": out}))
