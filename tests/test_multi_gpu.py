@@ -68,16 +68,19 @@ def test_autotuner_distinct_gpus():
         assert all(r["ok"].values()), r["ok"]
     assert res[0]["table"] == res[1]["table"]
     for e in res[0]["table"]:
-        assert e["ref"] == "rccl" or e["op"] in ("BAND", "BOR"), e
-        assert e["algo"] in ("rccl", "ipc"), e
+        if e["op"] in ("BAND", "BOR"):  # no RCCL op: the host transport is the reference engine
+            assert e["ref"] == "host" and e["algo"] in ("host", "ipc"), e
+        else:
+            assert e["ref"] == "rccl" and e["algo"] in ("rccl", "ipc"), e
 
 
-def test_group_churn_splits_distinct_gpus():
-    res = _run(W.group_churn, 2)
+@pytest.mark.parametrize("mode", ["share", "split"])
+def test_group_churn_distinct_gpus(mode):
+    res = _run(W.group_churn, 2, env={"PDCC_RCCL_GROUP_COMM": mode})
     for r in res:
         assert all(r["ok"]), r
         for g in r["groups"]:
-            assert g["how"] == ["split"], r
+            assert g["how"] == [mode], r
 
 
 @pytest.mark.parametrize("env", [{"PDCC_ALGO": "rccl"}, {"PDCC_ALGO": "ipc"}, {}])
