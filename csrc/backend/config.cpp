@@ -62,7 +62,10 @@ Config Config::from_env() {
   c.ipc_enable = env_bool("PDCC_IPC", c.ipc_enable);
   c.ipc_selftest = env_bool("PDCC_IPC_SELFTEST", c.ipc_selftest);
   c.ipc_selftest_ms = env_int("PDCC_IPC_SELFTEST_MS", c.ipc_selftest_ms);
-  c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
+  c.ipc_zc = env_bool("PDCC_IPC_ZC", c.ipc_zc);
+  c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
+  c.ipc_zc_cache = std::max<size_t>(1, env_size("PDCC_IPC_ZC_CACHE", c.ipc_zc_cache));
+  c.autotune =env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
   c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
   c.autotune_sample = std::max<size_t>(env_size("PDCC_AUTOTUNE_SAMPLE", c.autotune_sample), 64u << 10);
@@ -136,7 +139,8 @@ std::string Config::describe() const {
   o << "algo=" << algo_name(force_algo) << " ipc=" << ipc_enable << " ipc_selftest=" << ipc_selftest
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
-    << " ipc_max_staging=" << ipc_max_staging << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
+    << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")

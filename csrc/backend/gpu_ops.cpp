@@ -232,8 +232,9 @@ std::string members_key(const std::vector<int64_t>& global_ranks, int size) {
 
 // IPC self-test verdicts of earlier groups with the same member set on the same devices:
 // the topology did not change, so later groups skip the test when every rank has one.
+// '0' = no IPC, '1' = staged IPC only, '2' = staged and zero-copy IPC.
 std::mutex g_verdict_mu;
-std::map<std::string, bool> g_ipc_verdict;
+std::map<std::string, char> g_ipc_verdict;
 
 }  // namespace
 
@@ -305,7 +306,7 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
   {
     std::lock_guard<std::mutex> lk(g_verdict_mu);
     auto it = g_ipc_verdict.find(vkey);
-    if (it != g_ipc_verdict.end()) cached = it->second ? '1' : '0';
+    if (it != g_ipc_verdict.end()) cached = it->second;
   }
   const std::string mine = rec + "#" + cached;
   const auto all = store_allgather(store_, "pdcc/dev", rank_, size_, std::vector<uint8_t>(mine.begin(), mine.end()));
@@ -345,17 +346,19 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
     ds.ipc_ok = false;
   } else if (!cfg_.ipc_selftest) {
     ds.ipc_ok = true;
+    ds.zc_ok = cfg_.ipc_zc;
   } else if (all_cached) {
-    ds.ipc_ok = cached == '1';  // an earlier group with these members tested this topology
+    ds.ipc_ok = cached != '0';  // an earlier group with these members tested this topology
+    ds.zc_ok = cached == '2';
   } else {
     ds.ipc_ok = ipc_selftest(ds);
     std::lock_guard<std::mutex> lk(g_verdict_mu);
-    g_ipc_verdict[vkey] = ds.ipc_ok;
+    g_ipc_verdict[vkey] = !ds.ipc_ok ? '0' : ds.zc_ok ? '2' : '1';
   }
   ds.topo = true;
   if (cfg_.log_level >= 1)
-    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d shared_device=%d%s\n", rank_, d, bus,
-            (int)ds.rccl_ok, (int)ds.ipc_ok, (int)shared, all_cached ? " (cached IPC verdict)" : "");
+    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d zc_ok=%d shared_device=%d%s\n", rank_, d, bus,
+            (int)ds.rccl_ok, (int)ds.ipc_ok, (int)ds.zc_ok, (int)shared, all_cached ? " (cached IPC verdict)" : "");
 }
 
 RcclOpts ProcessGroupMI355X::rccl_opts() const {
@@ -445,7 +448,7 @@ IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
   if (!ds.ipc) {
     const uint64_t spin = (uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count()));
     auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging, spin,
-                                       ds.shared_device);
+                                       ds.shared_device, cfg_.ipc_zc_cache);
     std::lock_guard<std::mutex> lk(init_mu_);
     ds.ipc = c;
   }
@@ -473,7 +476,7 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
   bool ok = true;
   try {
     ds.ipc = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging,
-                                       (uint64_t)spin_ms, ds.shared_device);
+                                       (uint64_t)spin_ms, ds.shared_device, cfg_.ipc_zc_cache);
   } catch (const std::exception& e) {
     ok = false;
     why = e.what();
@@ -535,6 +538,89 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
     ds.ipc.reset();  // every rank voted after its own kernels finished: nothing touches these buffers any more
     return false;
   }
+  // zero-copy IPC (user buffers mapped per call and read in place): whole rows /
+  // tiles zero-copy plus a staged rest, twice on one buffer (first and cached
+  // mapping), all-gather with a ragged tail, reduce-scatter of a flat input
+  ds.zc_ok = false;
+  if (cfg_.ipc_zc) {
+    bool zok = true;
+    std::string zwhy;
+    IpcComm& ic = *ds.ipc;
+    try {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
+      const hipStream_t s = ds.stream.stream();
+      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+      const int64_t tile_f = kern::kTileBytes / 4;
+      const int64_t n = 3 * size_ * tile_f + 257;
+      const at::Tensor base = at::arange(n, opt).remainder(5);
+      at::Tensor x = base + (double)(rank_ + 1);
+      const double tri = size_ * (size_ + 1) / 2.0;
+      for (int k = 0; k < 2; ++k) {
+        kern::IpcCall c{};
+        c.coll = kern::IpcColl::ALLREDUCE_2SHOT;
+        c.dtype = kern::DType::F32;
+        c.op = kern::RedOp::SUM;
+        c.avg_div = size_;
+        c.bytes = x.nbytes();
+        c.in[0] = x.data_ptr();
+        c.out[0] = x.data_ptr();
+        ipc_run(ds, c, x.data_ptr(), x.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s,
+                k == 0 ? "pdcc/ipc_selftest/zc_ar0" : "pdcc/ipc_selftest/zc_ar1");
+        const at::Tensor want = k == 0 ? base * (double)size_ + tri : (base * (double)size_ + tri) * (double)size_;
+        zok = at::equal(x, want) && zok;
+      }
+      const int64_t m = 2 * tile_f + 5;
+      const at::Tensor in = at::full({m}, (double)rank_, opt);
+      at::Tensor out = at::full({m * size_}, -1.0, opt);
+      {
+        kern::IpcCall c{};
+        c.coll = kern::IpcColl::ALLGATHER;
+        c.dtype = kern::DType::U8;
+        c.op = kern::RedOp::COPY;
+        c.bytes = in.nbytes();
+        c.in[0] = in.data_ptr();
+        for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
+        ipc_run(ds, c, in.data_ptr(), in.nbytes(), kern::kTileBytes, ic.max_staging(), s, "pdcc/ipc_selftest/zc_ag");
+        zok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && zok;
+      }
+      {
+        const at::Tensor rin = at::arange(size_ * 2 * tile_f, opt).remainder(3) + (double)rank_;
+        at::Tensor rout = at::full({2 * tile_f}, -1.0, opt);
+        kern::IpcCall c{};
+        c.coll = kern::IpcColl::REDUCE_SCATTER;
+        c.dtype = kern::DType::F32;
+        c.op = kern::RedOp::SUM;
+        c.avg_div = size_;
+        c.bytes = rout.nbytes();
+        c.zstride = rout.nbytes();
+        for (int r = 0; r < size_; ++r) c.in[r] = static_cast<const char*>(rin.data_ptr()) + r * rout.nbytes();
+        c.out[0] = rout.data_ptr();
+        ipc_run(ds, c, rin.data_ptr(), rin.nbytes(), kern::kTileBytes, ic.max_staging(), s, "pdcc/ipc_selftest/zc_rs");
+        const at::Tensor mine = rin.narrow(0, rank_ * 2 * tile_f, 2 * tile_f) - (double)rank_;
+        zok = at::equal(rout, mine * (double)size_ + (size_ - 1) * size_ / 2.0) && zok;
+      }
+      PDCC_HIP(hipStreamSynchronize(s));
+      if (ic.error_word() != 0) {
+        zok = false;
+        zwhy = "a cross-GPU barrier timed out";
+        ic.clear_error();
+      } else if (!zok) {
+        zwhy = "wrong data";
+      }
+    } catch (const std::exception& e) {
+      zok = false;
+      zwhy = e.what();
+    }
+    if (const char* f = std::getenv("PDCC_IPC_ZC_SELFTEST_FAIL"))  // test hook: this rank reports a failure
+      if (*f && std::atoi(f) == rank_) {
+        zok = false;
+        zwhy = "PDCC_IPC_ZC_SELFTEST_FAIL";
+      }
+    ds.zc_ok = vote("pdcc/ipc_selftest/zc", zok);
+    if (!ds.zc_ok)
+      fprintf(stderr, "[pdcc r%d] zero-copy IPC self-test failed (%s): group '%s' stages every IPC call\n", rank_,
+              zok ? "on another rank" : zwhy.c_str(), group_name_.c_str());
+  }
   ds.ipc->set_timeout_ms((uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count())));
   return true;
 }
@@ -577,6 +663,79 @@ void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per
     }
     ic.launch(c, s);
   }
+}
+
+// Zero-copy IPC. Every step depends on group-wide facts or on the exchanged records
+// only, so all ranks take the same branch: the records go round the host transport
+// (a few us), a second round only when some rank exported an allocation its peers
+// have not mapped yet (agreeing that every mapping worked).
+size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen,
+                                         size_t unit, hipStream_t s, const char* selftest) {
+  if (!selftest && (!ds.zc_ok || !cfg_.ipc_zc || call.bytes < cfg_.ipc_zc_min)) return 0;
+  const size_t body = call.bytes / unit * unit;
+  if (body == 0) return 0;
+  IpcComm& ic = ds.ipc ? *ds.ipc : ipc(ds);
+  const bool cap = capturing(s);
+  const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, cap);
+  std::vector<IpcComm::ZcRec> all(size_);
+  if (selftest) {  // init_mu_ is held: exchange through the store, not the host transport
+    const auto v = store_allgather(store_, std::string(selftest) + "/rec", rank_, size_,
+                                   std::vector<uint8_t>(reinterpret_cast<const uint8_t*>(&mine),
+                                                        reinterpret_cast<const uint8_t*>(&mine) + sizeof(mine)));
+    for (int r = 0; r < size_; ++r) {
+      TORCH_CHECK(v[r].size() == sizeof(IpcComm::ZcRec), "pdcc: malformed zero-copy record");
+      std::memcpy(&all[r], v[r].data(), sizeof(IpcComm::ZcRec));
+    }
+  } else {
+    std::vector<void*> outs;
+    for (auto& r : all) outs.push_back(&r);
+    shm().allgather(&mine, outs, sizeof(mine), timeout_);
+  }
+  bool all_ok = true, fresh = false;
+  for (const auto& r : all) {
+    all_ok = all_ok && r.ok;
+    fresh = fresh || r.fresh;
+  }
+  std::vector<char*> ptrs;
+  bool ok = ic.zc_import(all, zbuf, all_ok, ptrs);
+  if (all_ok && fresh) {
+    if (selftest) {
+      const auto v = store_allgather(store_, std::string(selftest) + "/mapped", rank_, size_,
+                                     std::vector<uint8_t>{(uint8_t)ok});
+      for (const auto& x : v) ok = ok && !x.empty() && x[0] == 1;
+    } else {
+      double f = ok ? 1.0 : 0.0;
+      shm().allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
+      ok = f > 0.0;
+    }
+  }
+  ok = ok && all_ok;
+  ic.zc_settle(ok);
+  if (!ok) return 0;
+  call.bytes = body;
+  ic.launch_zc(call, ptrs, s);
+  return body;
+}
+
+void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
+                                 size_t per_call_max, hipStream_t s, const char* selftest) {
+  const size_t body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    zc_ran_ = body > 0;
+  }
+  if (body == call.bytes) return;
+  kern::IpcCall rest = call;
+  rest.bytes = call.bytes - body;
+  for (int k = 0; k < kern::kMaxRanks; ++k) {
+    if (call.in[k]) rest.in[k] = static_cast<const char*>(call.in[k]) + body;
+    if (call.out[k]) rest.out[k] = static_cast<char*>(call.out[k]) + body;
+  }
+  if (body && rest.bytes <= cfg_.ipc_1shot_max) {  // the rest of a zero-copy 2-shot is short
+    if (rest.coll == kern::IpcColl::ALLREDUCE_2SHOT) rest.coll = kern::IpcColl::ALLREDUCE_1SHOT;
+    if (rest.coll == kern::IpcColl::BROADCAST_2SHOT) rest.coll = kern::IpcColl::BROADCAST_1SHOT;
+  }
+  ipc_chunked(ipc(ds), rest, per_call_max, s);
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& ds,
@@ -881,7 +1040,12 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     c.bytes = w.nbytes();
     c.in[0] = w.data_ptr();
     c.out[0] = w.data_ptr();
-    ipc_chunked(ic, c, ic.max_staging(), s);
+    // all-reduce 2-shot reads the peers' tensors in place (a rooted reduce stays staged:
+    // its in-place phase 1 would overwrite non-root buffers)
+    if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT)
+      ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
+    else
+      ipc_chunked(ic, c, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
     RcclComm& rc = rccl(ds);
@@ -909,7 +1073,10 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
     c.bytes = bytes;
     c.in[0] = w.data_ptr();
     c.out[0] = w.data_ptr();
-    ipc_chunked(ic, c, ic.max_staging(), s);
+    if (c.coll == kern::IpcColl::BROADCAST_2SHOT)
+      ipc_run(ds, c, w.data_ptr(), bytes, (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
+    else
+      ipc_chunked(ic, c, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
     PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rccl(ds).get(), s));
   } else {
@@ -936,7 +1103,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
     c.in[0] = wi.data_ptr();
     if (receiver)
       for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
-    ipc_chunked(ic, c, ic.max_staging(), s);
+    ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     if (!rooted && is_flat(wo, bytes)) {
@@ -1034,9 +1201,12 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
     c.op = ko;
     c.avg_div = size_;
     c.bytes = bytes;
+    c.zstride = bytes;
     for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
     c.out[0] = wo.data_ptr();
-    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+    // a flat input (reduce_scatter_tensor) is read in place by every peer
+    ipc_run(ds, c, is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr, bytes * size_, kern::kTileBytes,
+            ic.max_staging() / size_, s);
   } else if (a == Algo::RCCL) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", wo.scalar_type());
     RcclComm& rc = rccl(ds);
@@ -1077,11 +1247,13 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
     c.dtype = kern::DType::U8;
     c.op = kern::RedOp::COPY;
     c.bytes = wi[0].nbytes();
+    c.zstride = c.bytes;
     for (int r = 0; r < size_; ++r) {
       c.in[r] = wi[r].data_ptr();
       c.out[r] = wo[r].data_ptr();
     }
-    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+    ipc_run(ds, c, is_flat(wi, c.bytes) ? wi[0].data_ptr() : nullptr, c.bytes * size_, kern::kTileBytes,
+            ic.max_staging() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     const size_t chunk = wi[0].nbytes();

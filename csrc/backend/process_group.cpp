@@ -531,12 +531,15 @@ void ProcessGroupMI355X::record_setup(const std::string& key, std::chrono::stead
 void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0) {
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> lk(stats_mu_);
-  const std::string key = std::string(coll_name(c)) + "/" + algo;
+  // an IPC op whose body ran zero-copy (ipc_run) is counted as "<algo>_zc"
+  const std::string name = std::string(algo) + (zc_ran_ && std::strncmp(algo, "ipc", 3) == 0 ? "_zc" : "");
+  zc_ran_ = false;
+  const std::string key = std::string(coll_name(c)) + "/" + name;
   OpStats& s = stats_[key];
   s.calls++;
   s.bytes += bytes;
   s.host_ms += ms;
-  last_algo_ = algo;
+  last_algo_ = name;
   if (fr_cap_ > 0) {
     FrEntry e{op_seq_.load(), key, bytes,
               std::chrono::duration<double, std::milli>(t0 - created_).count(), (bool)fr_last_work_,
@@ -591,8 +594,10 @@ std::string ProcessGroupMI355X::describe() {
   std::lock_guard<std::mutex> lk(init_mu_);
   for (auto& kv : devs_)
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
-      << ", shared_device=" << kv.second->shared_device << ", rccl=" << (kv.second->rccl != nullptr)
-      << ", ipc=" << (kv.second->ipc != nullptr) << "}";
+      << ", zc_ok=" << kv.second->zc_ok << ", shared_device=" << kv.second->shared_device
+      << ", rccl=" << (kv.second->rccl != nullptr) << ", ipc=" << (kv.second->ipc != nullptr)
+      << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
+      << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0) << "}";
   o << ")";
   return o.str();
 }

@@ -191,6 +191,7 @@ struct DeviceState {
   std::vector<std::string> recs;        // "host|pci bus" of every rank (topology exchange)
   bool rccl_ok = false;                 // all ranks on distinct devices
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
+  bool zc_ok = false;                   // zero-copy IPC (user buffers read in place) passed its self-test
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
   std::shared_ptr<IpcComm> ipc;         // lazy
@@ -334,6 +335,17 @@ class ProcessGroupMI355X : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> host_staged(Coll c, std::vector<at::Tensor> outputs,
                                              const std::function<void()>& fn);
   void ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per_call_max, hipStream_t s);
+  // Zero-copy IPC call (PDCC_IPC_ZC): every rank's `zbuf` (`zlen` readable bytes) is
+  // mapped into its peers and read in place. Runs the leading whole `unit`s of
+  // call.bytes and returns how many bytes that was (0 = nothing ran: the caller
+  // stages everything); the caller stages the rest. Collective over the group.
+  // `selftest` (a store key): run regardless of size / zc_ok, exchanging through the store.
+  size_t ipc_zero_copy(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
+                       hipStream_t s, const char* selftest = nullptr);
+  // Run `call` zero-copy where possible and the remainder (or everything) staged:
+  // the staged rest is the same call with every in/out pointer moved past the body.
+  void ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
+               size_t per_call_max, hipStream_t s, const char* selftest = nullptr);
 
   // p2p on CPU runs on two background threads (so isend/irecv pairs never deadlock)
   struct Job {
@@ -476,6 +488,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::mutex stats_mu_;
   std::map<std::string, OpStats> stats_;
   std::string last_algo_;
+  bool zc_ran_ = false;  // the last ipc_run ran its body zero-copy (consumed by record())
 
   std::mutex p2p_mu_;
   std::condition_variable p2p_cv_;

@@ -100,7 +100,7 @@ void check_blobs(const std::vector<std::vector<uint8_t>>& all, int self, const c
 }  // namespace
 
 IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world,
-                 int device, size_t max_staging, uint64_t timeout_ms, bool shared_device)
+                 int device, size_t max_staging, uint64_t timeout_ms, bool shared_device, size_t zc_cache)
     : store_(store),
       key_(key),
       rank_(rank),
@@ -109,6 +109,8 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       max_staging_(std::max<size_t>(max_staging, 1u << 20)),
       timeout_ticks_(timeout_ms * 100000ull),  // s_memrealtime runs at 100 MHz
       shared_device_(shared_device) {
+  zc_imports_.assign(world, {});
+  zc_cache_ = std::max<size_t>(zc_cache, 1);
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
   DeviceScope ds(device);
@@ -163,6 +165,10 @@ IpcComm::~IpcComm() {
       if (r.mine) hipFree(r.mine);
     }
     retired_.clear();
+    for (auto& peer : zc_imports_)
+      for (auto& im : peer)
+        if (im.map) hipIpcCloseMemHandle(im.map);
+    zc_imports_.clear();
     for (void* m : flags_maps_)
       if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
@@ -254,10 +260,14 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   // A captured graph bakes the staging pointers into its kernel arguments: from
   // now on staging is retired, never freed, when it grows.
   if (capturing) graph_mode_ = true;
+  call.zc = 0;
+  launch_view(view(peer_staging_), call, stream);
+}
+
+kern::IpcView IpcComm::view(const std::vector<char*>& bufs) const {
   kern::IpcView v{};
-  ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
   for (int r = 0; r < world_; ++r) {
-    v.buf[r] = peer_staging_.empty() ? nullptr : peer_staging_[r];
+    v.buf[r] = bufs.empty() ? nullptr : bufs[r];
     v.flags[r] = peer_flags_[r];
   }
   v.err = err_dev_;
@@ -268,6 +278,11 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   v.timeout_ticks = timeout_ticks_;
   v.trace = trace_dev_;
   v.trace_cap = trace_cap_;
+  return v;
+}
+
+void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_t stream) {
+  ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
   if (shared_device_) {
     // all ranks' grids must be co-resident on ONE device (test setups): stay well
     // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
@@ -275,6 +290,131 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   }
   DeviceScope ds(device_);
   PDCC_HIP(kern::ipc_launch(v, call, stream));
+}
+
+// ------------------------------------------------------------------ zero copy
+IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
+  ZcRec r{};
+  zc_pending_ = false;
+  if (!p || len == 0 || (reinterpret_cast<uintptr_t>(p) & 15u) != 0) return r;
+  DeviceScope ds(device_);
+  hipDeviceptr_t base = nullptr;
+  size_t range = 0;
+  if (hipMemGetAddressRange(&base, &range, reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))) != hipSuccess) {
+    (void)hipGetLastError();
+    return r;
+  }
+  const uint64_t off = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<char*>(base));
+  if (off + len > range) return r;  // the readable span must lie inside one allocation
+  uint64_t id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base) != hipSuccess || id == 0) {
+    (void)hipGetLastError();
+    return r;
+  }
+  auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(),
+                         [&](const ZcExport& e) { return e.id == id && e.base == static_cast<char*>(base); });
+  if (it == zc_exports_.end()) {
+    ZcExport e{};
+    e.id = id;
+    e.base = static_cast<char*>(base);
+    if (hipIpcGetMemHandle(&e.handle, base) != hipSuccess) {
+      (void)hipGetLastError();  // e.g. a range the runtime refuses to export (ranks sharing a device)
+      return r;
+    }
+    // LRU eviction (never while capturing: importers could not drain their streams
+    // before unmapping, and the graph may hold the pointers)
+    if (zc_exports_.size() >= zc_cache_ && !capturing) {
+      auto victim = zc_exports_.end();
+      for (auto v = zc_exports_.begin(); v != zc_exports_.end(); ++v)
+        if (!v->pinned && (victim == zc_exports_.end() || v->last < victim->last)) victim = v;
+      if (victim != zc_exports_.end()) {
+        r.evict = victim->id;
+        zc_exports_.erase(victim);
+      }
+    }
+    zc_exports_.push_back(e);
+    it = zc_exports_.end() - 1;
+  }
+  it->last = ++zc_tick_;
+  if (capturing) it->pinned = true;
+  r.ok = 1;
+  r.fresh = it->confirmed ? 0 : 1;
+  r.id = id;
+  r.off = off;
+  r.len = len;
+  r.handle = it->handle;
+  if (r.fresh) {
+    zc_pending_ = true;
+    zc_pending_id_ = id;
+  }
+  return r;
+}
+
+bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
+  DeviceScope ds(device_);
+  // evictions first, whatever the outcome of this exchange (keeps the caches in step)
+  bool drained = false;
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_ || all[r].evict == 0) continue;
+    auto& peer = zc_imports_[r];
+    auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].evict; });
+    if (it == peer.end()) continue;
+    if (!drained) {  // an in-flight kernel of this rank may still read through the mapping
+      PDCC_HIP(hipDeviceSynchronize());
+      drained = true;
+    }
+    hipIpcCloseMemHandle(it->map);
+    peer.erase(it);
+  }
+  if (!all_ok) return false;
+  ptrs.assign(world_, nullptr);
+  bool ok = true;
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) {
+      ptrs[r] = static_cast<char*>(const_cast<void*>(mine));
+      continue;
+    }
+    auto& peer = zc_imports_[r];
+    auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].id; });
+    if (it == peer.end()) {
+      void* m = nullptr;
+      if (hipIpcOpenMemHandle(&m, all[r].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !m) {
+        (void)hipGetLastError();
+        if (!all[r].fresh)  // every rank mapped it when it was fresh: this cannot be agreed on any more
+          throw std::runtime_error("pdcc: zero-copy IPC: re-mapping a confirmed peer buffer failed on rank " +
+                                   std::to_string(rank_));
+        ok = false;
+        continue;
+      }
+      peer.push_back({all[r].id, m});
+      it = peer.end() - 1;
+    }
+    ptrs[r] = static_cast<char*>(it->map) + all[r].off;
+  }
+  return ok;
+}
+
+void IpcComm::zc_settle(bool ok) {
+  if (!zc_pending_) return;
+  auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(),
+                         [&](const ZcExport& e) { return e.id == zc_pending_id_; });
+  if (it != zc_exports_.end()) {
+    if (ok) it->confirmed = true;
+    else if (!it->pinned) zc_exports_.erase(it);  // announced fresh again next time
+  }
+  zc_pending_ = false;
+}
+
+void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream) {
+  if ((int)bufs.size() != world_) throw std::runtime_error("pdcc: zero-copy IPC launch without every rank's buffer");
+  call.zc = 1;
+  launch_view(view(bufs), call, stream);
+}
+
+size_t IpcComm::zc_mappings() const {
+  size_t n = 0;
+  for (const auto& p : zc_imports_) n += p.size();
+  return n;
 }
 
 uint32_t IpcComm::error_word() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0u; }

@@ -31,7 +31,7 @@ class IpcComm {
  public:
   // Collective: allocate own signal area + error word and exchange handles.
   IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world, int device,
-          size_t max_staging, uint64_t timeout_ms, bool shared_device);
+          size_t max_staging, uint64_t timeout_ms, bool shared_device, size_t zc_cache = 16);
   ~IpcComm();
   IpcComm(const IpcComm&) = delete;
   IpcComm& operator=(const IpcComm&) = delete;
@@ -66,9 +66,62 @@ class IpcComm {
   int world() const { return world_; }
   uint64_t calls() const { return seq_; }
 
+  // ---- zero-copy calls: the peers read this call's USER buffers in place ----------
+  // One rank's buffer, exchanged over the host transport before the launch (the
+  // caller drives the exchange; every rank runs the same steps):
+  //   rec = zc_export(p, len)  ->  all-gather recs  ->  zc_import(all, ...)  ->
+  //   [fresh anywhere: agree on the import result]  ->  zc_settle(ok)  ->  launch_zc.
+  // `id` is the exporter's allocation id (HIP BUFFER_ID): an allocation freed and
+  // re-made at the same address gets a new one, so nobody reads through a stale
+  // mapping. Importers keep a mapping until its exporter evicts it (`evict`, LRU
+  // over PDCC_IPC_ZC_CACHE exports), so all caches stay in step without extra
+  // messages; exports made while capturing a graph are pinned (the graph keeps
+  // the pointers) and never evicted.
+  struct ZcRec {
+    uint8_t ok;     // 1 = exportable: 16-B aligned, inside one allocation, handle obtained
+    uint8_t fresh;  // 1 = the peers have not confirmed a mapping of `id` yet
+    uint8_t pad[6];
+    uint64_t id;
+    uint64_t evict;  // allocation id the exporter dropped (0 = none): importers unmap it
+    uint64_t off;    // byte offset of the buffer in its allocation
+    uint64_t len;    // readable bytes at the buffer
+    hipIpcMemHandle_t handle;
+  };
+  ZcRec zc_export(const void* p, size_t len, bool capturing);
+  // Apply every peer's eviction, then (all_ok) map every rank's buffer: ptrs[r]
+  // (own = `mine`). False if a mapping failed on this rank.
+  bool zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs);
+  // group-wide outcome of this exchange: this rank's fresh export is confirmed or dropped
+  void zc_settle(bool ok);
+  // one zero-copy launch (call.zc is set here); bufs[r] = rank r's mapped buffer
+  void launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream);
+  size_t zc_exports() const { return zc_exports_.size(); }
+  size_t zc_mappings() const;
+
  private:
   void map_staging(size_t cap);
   void unmap_staging();
+  kern::IpcView view(const std::vector<char*>& bufs) const;
+  void launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_t stream);
+
+  struct ZcExport {
+    uint64_t id;
+    char* base;
+    hipIpcMemHandle_t handle;
+    bool confirmed;
+    bool pinned;
+    uint64_t last;  // LRU tick
+  };
+  struct ZcImport {
+    uint64_t id;
+    void* map;  // hipIpcOpenMemHandle result (allocation base on this side)
+  };
+  std::vector<ZcExport> zc_exports_;
+  std::vector<std::vector<ZcImport>> zc_imports_;  // per peer
+  size_t zc_cache_ = 16;
+  uint64_t zc_tick_ = 0;
+  bool zc_pending_ = false;  // an export was announced fresh in the exchange in progress ...
+  uint64_t zc_pending_id_ = 0;  // ... this one
 
   c10::intrusive_ptr<c10d::Store> store_;
   std::string key_;

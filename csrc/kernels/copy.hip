@@ -63,6 +63,52 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 }
 
 // ----------------------------------------------------------- IPC copy family
+// Zero-copy copies (IpcCall::zc): peers' user buffers are read in place; data
+// arrival barrier first, departure barrier last (see ipc_reduce_zc).
+template <int W>
+__device__ __forceinline__ void ipc_copy_zc(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr,
+                                            uint32_t ep) {
+  const size_t G = gridDim.x, b = blockIdx.x;
+  const int me = v.rank;
+  const size_t nt = c.bytes / kTile;
+  block_barrier(v, ep);
+  tr.mark(2);
+  tr.mark(4);
+  switch (c.coll) {
+    case IpcColl::BROADCAST_2SHOT: {
+      if (me != c.root) {  // phase 1: my owned tiles straight from the root's buffer into mine
+        const OneSrcMap m{v.buf[c.root], v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      tr.mark(5);
+      block_barrier(v, ep + 2u);
+      tr.mark(6);
+      if (me != c.root) {  // phase 2: the other owners' tiles (the root's own straight from the root)
+        const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      break;
+    }
+    case IpcColl::ALLGATHER:
+    case IpcColl::GATHER:
+      if (c.coll == IpcColl::ALLGATHER || me == c.root) {
+        const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(me + b), b, G, nt};
+        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+      tr.mark(5);
+      break;
+    case IpcColl::ALLTOALL: {
+      const PeerTileMap<W> m{&v, &c, (size_t)me * c.zstride, c.bytes, (uint32_t)(me + b), b, G, nt};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      tr.mark(5);
+      break;
+    }
+    default:
+      break;
+  }
+  block_barrier<false>(v, ep + 3u);  // departure
+}
+
 template <int W>
 __device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
   const size_t G = gridDim.x, b = blockIdx.x;
@@ -72,6 +118,10 @@ __device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
   if (c.coll == IpcColl::BARRIER) {  // the arrival barrier is the whole collective
     block_barrier<false>(v, ep);
+    return;
+  }
+  if (c.zc) {
+    ipc_copy_zc<W>(v, c, lds, tr, ep);
     return;
   }
   block_barrier<false>(v, ep);  // arrival: every peer's previous call is over
@@ -260,6 +310,7 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 size_t ipc_signal_bytes() { return (size_t)(kCountWord + kMaxBlocks) * sizeof(uint32_t); }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
+  if (c.zc) return 0;  // peers read the user buffers in place
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
   switch (c.coll) {
     case IpcColl::SCATTER:
@@ -283,6 +334,13 @@ size_t ipc_staging_bytes(const IpcCall& c, int world) {
 hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream) {
   IpcCall c = call;
   if (v.world < 2 || v.world > kMaxRanks) return hipErrorInvalidValue;
+  if (c.zc) {  // in-place reads of user buffers: whole tiles (2-shot: whole rows of W tiles), no over-read
+    const bool rows = c.coll == IpcColl::ALLREDUCE_2SHOT || c.coll == IpcColl::BROADCAST_2SHOT;
+    const bool known = rows || c.coll == IpcColl::ALLGATHER || c.coll == IpcColl::GATHER ||
+                       c.coll == IpcColl::REDUCE_SCATTER || c.coll == IpcColl::ALLTOALL;
+    const size_t unit = (size_t)kTileBytes * (rows ? v.world : 1);
+    if (!known || c.bytes == 0 || c.bytes % unit != 0) return hipErrorInvalidValue;
+  }
   const size_t nt = (c.bytes + kTileBytes - 1) / kTileBytes;
   int grid = c.grid;
   if (grid <= 0) {

@@ -116,6 +116,16 @@ enum class IpcColl : int32_t {
 
 // Arguments of one IPC collective. `chunk_bytes` is the per-rank payload of one
 // chunk (all-gather/scatter/... operate on W chunks of that size).
+//
+// Zero-copy calls (`zc` = 1): IpcView::buf[r] is rank r's USER buffer of this call
+// (mapped for the call by IpcComm::zc_*), read in place -- no staging copy. Then
+//   ALLREDUCE_2SHOT   buf[r] = rank r's tensor (in = out); bytes = whole rows of W tiles
+//   BROADCAST_2SHOT   buf[r] = rank r's tensor;             bytes = whole rows of W tiles
+//   ALLGATHER/GATHER  buf[r] = rank r's input;              bytes = whole tiles
+//   REDUCE_SCATTER    buf[r] = rank r's flat input, chunk q at q * zstride; bytes = whole tiles
+//   ALLTOALL          buf[r] = rank r's flat input, chunk q at q * zstride; bytes = whole tiles
+// and every call ends with a departure barrier (no peer reads my buffer any more
+// once my kernel is done, so the caller may overwrite or free it).
 struct IpcCall {
   IpcColl coll;
   DType dtype;
@@ -124,7 +134,9 @@ struct IpcCall {
   int avg_div;
   int grid;                      // 0 = pick
   int grid_cap;                  // > 0: upper bound on the picked grid (co-residency on shared devices)
+  int zc;                        // 1 = zero-copy call (see above)
   size_t bytes;                  // payload bytes (per rank / per chunk, see above)
+  size_t zstride;                // zero-copy chunked inputs: byte distance between chunks
   const void* in[kMaxRanks];     // local inputs: in[0] for single-tensor inputs, in[c] per chunk for lists
   void* out[kMaxRanks];          // local outputs: out[0] single, out[c] per chunk for lists
 };

@@ -165,6 +165,33 @@ struct OwnerRowMap {
   }
 };
 
+// Zero-copy 2-shot phase 2 (IpcCall::zc): the W-1 tiles of each row that OTHER ranks
+// own -- the own tiles were reduced (or fetched) in place in phase 1. Rows first +
+// stride*k, owners rotated per item, row and block like OwnerRowMap. Rows are whole.
+template <int W>
+struct PeerRowMap {
+  const IpcView* v;
+  char* d;
+  uint32_t rot;
+  size_t first, stride, nrows;
+  __device__ size_t count() const { return first < nrows ? ((nrows - 1 - first) / stride + 1) * (W - 1) : 0; }
+  __device__ size_t tile(size_t i, int& q) const {
+    const uint32_t k = (uint32_t)i / (W - 1), j = (uint32_t)i - k * (W - 1);
+    q = (v->rank + 1 + (int)((rot + j + k) % (W - 1))) % W;
+    return (size_t)q + (size_t)W * (first + stride * k);
+  }
+  __device__ const char* src(int, size_t i) const {
+    int q;
+    const size_t t = tile(i, q);
+    return v->buf[q] + t * kTile;
+  }
+  __device__ char* dst(size_t i) const {
+    int q;
+    return d + tile(i, q) * kTile;
+  }
+  __device__ size_t valid(size_t) const { return kTile; }
+};
+
 // all-gather / gather / all-to-all: (tile t of this block, source rank q) pairs;
 // source q's tile lives at v->buf[q] + sbase + t*kTile and lands in out[q].
 template <int W>
@@ -198,6 +225,42 @@ struct PeerTileMap {
   }
 };
 
+// Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
+// The arrival barrier is a data barrier here -- it hands over each rank's input,
+// written by the kernels before this one -- and a departure barrier ends the call:
+// once it passes, no peer reads this rank's buffer any more (the caller may reuse it).
+// Phase 1 of the all-reduce writes the reduced own tiles in place: peers only ever
+// read tiles they own there, and those are not written by this rank.
+template <DType DT, RedOp OP, int W>
+__device__ __forceinline__ void ipc_reduce_zc(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr,
+                                              uint32_t ep) {
+  constexpr int D = DepthFor<W>::value;
+  const size_t G = gridDim.x, b = blockIdx.x;
+  const int me = v.rank;
+  const size_t nt = c.bytes / kTile;
+  block_barrier(v, ep);
+  tr.mark(2);
+  tr.mark(4);
+  if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
+    {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
+      const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+    }
+    tr.mark(5);
+    block_barrier(v, ep + 2u);
+    tr.mark(6);
+    {  // phase 2: the other owners' reduced tiles
+      const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+    }
+  } else if (c.coll == IpcColl::REDUCE_SCATTER) {
+    const AllSrcMap<W> m{&v, (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
+    pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+    tr.mark(5);
+  }
+  block_barrier<false>(v, ep + 3u);  // departure
+}
+
 template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
   constexpr int D = DepthFor<W>::value;
@@ -206,6 +269,10 @@ __device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall&
   const uint32_t seq = block_seq(v);
   tr.seq(seq);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
+  if (c.zc) {
+    ipc_reduce_zc<DT, OP, W>(v, c, lds, tr, ep);
+    return;
+  }
   block_barrier<false>(v, ep);  // arrival: every peer's previous call is over
   tr.mark(2);
   const size_t poff = 0;        // single staging buffer (the arrival barrier guards reuse)

@@ -72,6 +72,9 @@ class Config:
     ipc_2shot_max: int = 8 << 20
     ipc_copy_max: int = 1 << 20
     ipc_max_staging: int = 1 << 30
+    ipc_zc: bool = True
+    ipc_zc_min: int = 1 << 20
+    ipc_zc_cache: int = 16
     ipc_spin_ms: int = 600000
     autotune: bool = True
     autotune_min: int = 64 << 10
@@ -103,7 +106,8 @@ _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_selftest": "PDCC_IPC_SELFTEST",
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
-    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "autotune": "PDCC_AUTOTUNE",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_zc_min": "PDCC_IPC_ZC_MIN",
+    "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",

@@ -40,6 +40,13 @@ for s in "$@"; do
     graphprobe_q1) GPU_MAX_HW_QUEUES=1 step graphprobe_q1 300 python scripts/graph_probe.py ;;
     graphprof) step graphprof 400 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$0/gpurun_out/prof_graph" -o g -- python3 "$0/scripts/graph_bench.py"' "$(pwd)" ;;
+    zcbench) step zcbench 400 python scripts/zc_bench.py ;;
+    zcbench4) step zcbench4 400 python scripts/zc_bench.py --world 4 --sizes 4M,64M ;;
+    zcprobe) step zcprobe 120 python scripts/ipc_buffer_probe.py ;;
+    zctest) step zctest 600 python -u -m pytest tests/test_backend_gpu.py -x -v --timeout 300 --timeout-method thread \
+        -k "zero_copy or selftest or bulk or golden" ;;
+    zcprof) step zcprof 500 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$0/gpurun_out/prof_zc" -o zc -- python3 "$0/scripts/zc_bench.py" --sizes 64M --iters 8' "$(pwd)" ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;

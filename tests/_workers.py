@@ -820,3 +820,75 @@ def lifecycle_probe(rank, size, device="cpu"):
     dist.destroy_process_group(h)
     ok["healthy_flag"] = be.native_backend().healthy()
     return ok
+
+
+def zero_copy(rank, size, device="cuda"):
+    """Zero-copy IPC (PDCC_ALGO=ipc, PDCC_IPC_ZC on): the peers read each rank's own
+    tensor in place. Sizes with and without a staged rest, one buffer reused (cached
+    mappings), fresh allocations past the export cache with empty_cache() in between
+    (eviction, allocations re-made at the same address), every zero-copy collective,
+    and a rank-asymmetric layout (one rank's reduce_scatter input not flat: the group
+    agrees to stage). Returns {check: bool}."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    ok = {}
+    tile = 1024  # fp32 elements per 4 KiB tile
+    tri = size * (size + 1) // 2
+    for n in (size * tile * 300, size * tile * 300 + 77, (1 << 20) // 4 + 3, 3 * size * tile * 256 + 1):
+        base = torch.arange(n, device=d, dtype=torch.float32) % 1000
+        t = base * (rank + 1)
+        dist.all_reduce(t)
+        ok[f"all_reduce_{n}"] = bool(torch.equal(t, base * tri))
+    x = torch.empty(size * tile * 256, device=d)
+    for _ in range(10):
+        x.fill_(rank + 1.0)
+        dist.all_reduce(x)
+    ok["reuse"] = bool(torch.all(x == tri))
+    good = True
+    for i in range(40):  # > PDCC_IPC_ZC_CACHE distinct allocations
+        y = torch.full((tile * 512 + i * size * tile,), float(rank + i), device=d)
+        dist.all_reduce(y)
+        good = good and bool(torch.all(y == sum(r + i for r in range(size))))
+        del y
+        if i % 8 == 7:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    ok["churn"] = good
+    m = tile * 300 + 5
+    src = torch.full((m,), float(rank), device=d)
+    out = torch.empty(size * m, device=d)
+    dist.all_gather_into_tensor(out, src)
+    ok["all_gather_into_tensor"] = bool(torch.equal(out, torch.arange(size, device=d).float().repeat_interleave(m)))
+    lst = [torch.empty(m + 64, device=d)[:m] for _ in range(size)]
+    dist.all_gather(lst, src)
+    ok["all_gather_list"] = all(bool(torch.all(v == q)) for q, v in enumerate(lst))
+    inp = torch.arange(size * m, dtype=torch.float32, device=d) % 97 + rank
+    o = torch.empty(m, device=d)
+    dist.reduce_scatter_tensor(o, inp)
+    exp = ((torch.arange(size * m, dtype=torch.float32, device=d) % 97) * size + size * (size - 1) / 2)
+    ok["reduce_scatter_tensor"] = bool(torch.equal(o, exp[rank * m:(rank + 1) * m]))
+    a2a_in = torch.arange(size * m, dtype=torch.float32, device=d) + 10000 * rank
+    a2a_out = torch.empty_like(a2a_in)
+    dist.all_to_all_single(a2a_out, a2a_in)
+    exp = torch.cat([torch.arange(rank * m, (rank + 1) * m, dtype=torch.float32, device=d) + 10000 * q
+                     for q in range(size)])
+    ok["all_to_all_single"] = bool(torch.equal(a2a_out, exp))
+    b = torch.arange(size * tile * 200 + 9, dtype=torch.float32, device=d) if rank == 1 else \
+        torch.zeros(size * tile * 200 + 9, device=d)
+    dist.broadcast(b, src=1)
+    ok["broadcast"] = bool(torch.equal(b, torch.arange(b.numel(), dtype=torch.float32, device=d)))
+    m2 = tile * 260
+    full = torch.arange(size * m2, dtype=torch.float32, device=d)
+    ins = list(full.chunk(size)) if rank == 0 else [full[q * m2:(q + 1) * m2].clone() for q in range(size)]
+    o2 = torch.empty(m2, device=d)
+    dist.reduce_scatter(o2, ins)
+    ok["asymmetric_layout"] = bool(torch.equal(o2, full[rank * m2:(rank + 1) * m2] * size))
+    st = be.stats()
+    ok["zc_rows"] = any(k.endswith("_zc") for k in st)
+    ok["zc_ok"] = "zc_ok=1" in be.describe()
+    dist.barrier()
+    return ok

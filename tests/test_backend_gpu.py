@@ -70,6 +70,22 @@ def test_shared_gpu_ipc_bulk(world, oneshot_max):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world,cache", [(2, "16"), (3, "4")])
+def test_shared_gpu_zero_copy(world, cache):
+    # peers read each rank's own tensor in place (no staging copy); cache 4 forces evictions
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": cache, "PDCC_IPC_1SHOT_MAX": "256K"}
+    for ok in _gpu_launch(W.zero_copy, world, env=env):
+        assert all(ok.values()), ok
+
+
+def test_zero_copy_selftest_gate():
+    # a failed zero-copy self-test leaves the staged IPC path on (and every result right)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_SELFTEST_FAIL": "1"}
+    for ok in _gpu_launch(W.zero_copy, 2, env=env):
+        assert ok.pop("zc_ok") is False and ok.pop("zc_rows") is False, ok
+        assert all(ok.values()), ok
+
+
 def test_shared_gpu_noncontig():
     for ok in _gpu_launch(W.noncontig, 2, env={"PDCC_ALGO": "ipc"}):
         assert all(ok.values()), ok
