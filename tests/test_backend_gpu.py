@@ -178,7 +178,10 @@ def test_autotuner_every_collective_shared_gpu():
 
 
 def test_autotune_ipc_timeout_is_contained():
-    env = {"PDCC_TEST_AUTOTUNE_DELAY": "1:1500", "PDCC_AUTOTUNE_SPIN_MS": "300", "PDCC_AUTOTUNE_COLLS": "allreduce"}
+    # the delay hook makes rank 1's host late; a zero-copy call would line the hosts up in its
+    # handle exchange before any kernel spins, so the staged protocol is the one under test
+    env = {"PDCC_TEST_AUTOTUNE_DELAY": "1:1500", "PDCC_AUTOTUNE_SPIN_MS": "300", "PDCC_AUTOTUNE_COLLS": "allreduce",
+           "PDCC_IPC_ZC": "0"}
     res = _gpu_launch(W.autotune_fault_probe, 2, env=env)
     for r in res:
         assert all(r["ok"]), r
