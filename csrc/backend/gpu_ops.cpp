@@ -712,6 +712,19 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
   ok = ok && all_ok;
   ic.zc_settle(ok);
   if (!ok) return 0;
+  if (call.coll == kern::IpcColl::REDUCE_2SHOT) {
+    // the rooted reduce stages its reduced tiles: chunks of at most the staging cap
+    const size_t chunk = std::max(unit, ic.max_staging() / unit * unit);
+    for (size_t off = 0; off < body; off += chunk) {
+      kern::IpcCall c = call;
+      c.bytes = std::min(chunk, body - off);
+      std::vector<char*> p = ptrs;
+      for (auto& q : p)
+        if (q) q += off;
+      ic.launch_zc(c, p, s);
+    }
+    return body;
+  }
   call.bytes = body;
   ic.launch_zc(call, ptrs, s);
   return body;
@@ -733,6 +746,7 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
   }
   if (body && rest.bytes <= cfg_.ipc_1shot_max) {  // the rest of a zero-copy 2-shot is short
     if (rest.coll == kern::IpcColl::ALLREDUCE_2SHOT) rest.coll = kern::IpcColl::ALLREDUCE_1SHOT;
+    if (rest.coll == kern::IpcColl::REDUCE_2SHOT) rest.coll = kern::IpcColl::REDUCE_1SHOT;
     if (rest.coll == kern::IpcColl::BROADCAST_2SHOT) rest.coll = kern::IpcColl::BROADCAST_1SHOT;
   }
   ipc_chunked(ipc(ds), rest, per_call_max, s);
@@ -1040,9 +1054,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     c.bytes = w.nbytes();
     c.in[0] = w.data_ptr();
     c.out[0] = w.data_ptr();
-    // all-reduce 2-shot reads the peers' tensors in place (a rooted reduce stays staged:
-    // its in-place phase 1 would overwrite non-root buffers)
-    if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT)
+    // 2-shot reads the peers' tensors in place (all-reduce: reduced in place too;
+    // rooted reduce: into staging, so non-root tensors stay untouched)
+    if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT || c.coll == kern::IpcColl::REDUCE_2SHOT)
       ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
     else
       ipc_chunked(ic, c, ic.max_staging(), s);
@@ -1157,10 +1171,13 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
     c.op = kern::RedOp::COPY;
     c.root = root;
     c.bytes = bytes;
+    c.zstride = bytes;
     if (rank_ == root)
       for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
     c.out[0] = wo.data_ptr();
-    ipc_chunked(ic, c, ic.max_staging() / size_, s);
+    // a flat root list (e.g. x.chunk(W)) is read in place; the other ranks share nothing
+    const void* z = rank_ == root ? (is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr) : nullptr;
+    ipc_run(ds, c, z, rank_ == root ? bytes * size_ : 0, kern::kTileBytes, ic.max_staging() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     PDCC_NCCL(ncclGroupStart());

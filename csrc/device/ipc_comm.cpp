@@ -245,6 +245,12 @@ void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
 }
 
 void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
+  call.zc = 0;
+  prepare_staging(call, stream);
+  launch_view(view(peer_staging_), call, stream);
+}
+
+void IpcComm::prepare_staging(const kern::IpcCall& call, hipStream_t stream) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   PDCC_HIP(hipStreamIsCapturing(stream, &cs));
   const bool capturing = cs != hipStreamCaptureStatusNone;
@@ -260,14 +266,13 @@ void IpcComm::launch(kern::IpcCall call, hipStream_t stream) {
   // A captured graph bakes the staging pointers into its kernel arguments: from
   // now on staging is retired, never freed, when it grows.
   if (capturing) graph_mode_ = true;
-  call.zc = 0;
-  launch_view(view(peer_staging_), call, stream);
 }
 
 kern::IpcView IpcComm::view(const std::vector<char*>& bufs) const {
   kern::IpcView v{};
   for (int r = 0; r < world_; ++r) {
     v.buf[r] = bufs.empty() ? nullptr : bufs[r];
+    v.stg[r] = peer_staging_.empty() ? nullptr : peer_staging_[r];
     v.flags[r] = peer_flags_[r];
   }
   v.err = err_dev_;
@@ -296,6 +301,10 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
 IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   ZcRec r{};
   zc_pending_ = false;
+  if (!p && len == 0) {  // this rank has nothing the peers read (a scatter's non-root)
+    r.ok = 1;
+    return r;
+  }
   if (!p || len == 0 || (reinterpret_cast<uintptr_t>(p) & 15u) != 0) return r;
   DeviceScope ds(device_);
   hipDeviceptr_t base = nullptr;
@@ -374,6 +383,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
       ptrs[r] = static_cast<char*>(const_cast<void*>(mine));
       continue;
     }
+    if (all[r].id == 0) continue;  // nothing to read from this rank
     auto& peer = zc_imports_[r];
     auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].id; });
     if (it == peer.end()) {
@@ -408,6 +418,7 @@ void IpcComm::zc_settle(bool ok) {
 void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream) {
   if ((int)bufs.size() != world_) throw std::runtime_error("pdcc: zero-copy IPC launch without every rank's buffer");
   call.zc = 1;
+  prepare_staging(call, stream);  // (a rooted reduce stages its reduced tiles)
   launch_view(view(bufs), call, stream);
 }
 

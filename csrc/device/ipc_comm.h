@@ -87,6 +87,7 @@ class IpcComm {
     uint64_t len;    // readable bytes at the buffer
     hipIpcMemHandle_t handle;
   };
+  // (p, len) = (nullptr, 0): this rank shares nothing (ok = 1, id = 0)
   ZcRec zc_export(const void* p, size_t len, bool capturing);
   // Apply every peer's eviction, then (all_ok) map every rank's buffer: ptrs[r]
   // (own = `mine`). False if a mapping failed on this rank.
@@ -102,6 +103,8 @@ class IpcComm {
   void map_staging(size_t cap);
   void unmap_staging();
   kern::IpcView view(const std::vector<char*>& bufs) const;
+  // grow the staging for `call` if needed (refused while the stream is being captured)
+  void prepare_staging(const kern::IpcCall& call, hipStream_t stream);
   void launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_t stream);
 
   struct ZcExport {

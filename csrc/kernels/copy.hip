@@ -103,6 +103,12 @@ __device__ __forceinline__ void ipc_copy_zc(const IpcView& v, const IpcCall& c, 
       tr.mark(5);
       break;
     }
+    case IpcColl::SCATTER: {  // my chunk straight out of the root's flat list
+      const OneSrcMap m{v.buf[c.root] + (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      tr.mark(5);
+      break;
+    }
     default:
       break;
   }
@@ -154,7 +160,7 @@ __device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c
       block_barrier(v, ph1);
       if (me == c.root) return;
       {  // phase 2: every owner's tiles, owners interleaved (all links at once)
-        const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
+        const OwnerRowMap<W> m{v.buf, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
@@ -310,7 +316,8 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 size_t ipc_signal_bytes() { return (size_t)(kCountWord + kMaxBlocks) * sizeof(uint32_t); }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
-  if (c.zc) return 0;  // peers read the user buffers in place
+  if (c.zc)  // peers read the user buffers in place; a rooted reduce stages its reduced tiles
+    return c.coll == IpcColl::REDUCE_2SHOT ? (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes : 0;
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
   switch (c.coll) {
     case IpcColl::SCATTER:
@@ -335,9 +342,11 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   IpcCall c = call;
   if (v.world < 2 || v.world > kMaxRanks) return hipErrorInvalidValue;
   if (c.zc) {  // in-place reads of user buffers: whole tiles (2-shot: whole rows of W tiles), no over-read
-    const bool rows = c.coll == IpcColl::ALLREDUCE_2SHOT || c.coll == IpcColl::BROADCAST_2SHOT;
+    const bool rows = c.coll == IpcColl::ALLREDUCE_2SHOT || c.coll == IpcColl::BROADCAST_2SHOT ||
+                      c.coll == IpcColl::REDUCE_2SHOT;
     const bool known = rows || c.coll == IpcColl::ALLGATHER || c.coll == IpcColl::GATHER ||
-                       c.coll == IpcColl::REDUCE_SCATTER || c.coll == IpcColl::ALLTOALL;
+                       c.coll == IpcColl::SCATTER || c.coll == IpcColl::REDUCE_SCATTER ||
+                       c.coll == IpcColl::ALLTOALL;
     const size_t unit = (size_t)kTileBytes * (rows ? v.world : 1);
     if (!known || c.bytes == 0 || c.bytes % unit != 0) return hipErrorInvalidValue;
   }

@@ -80,7 +80,8 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 constexpr int kCountWord = kMaxBlocks * kMaxRanks;  // u32 index of counters[0] in the signal area
 constexpr int kEpochsPerCall = 4;                   // arrival, data, second data phase (+1 spare)
 struct IpcView {
-  char* buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes
+  char* buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes; zero-copy: user buffers
+  char* stg[kMaxRanks];        // staging buffer per rank (zero-copy calls that still stage results)
   uint32_t* flags[kMaxRanks];  // signal area (uncached device memory) per rank
   uint32_t* err;               // host-mapped error word (0 = ok), written on spin timeout
   uint32_t* counters;          // own signal area + kCountWord: per-block call counters
@@ -120,12 +121,15 @@ enum class IpcColl : int32_t {
 // Zero-copy calls (`zc` = 1): IpcView::buf[r] is rank r's USER buffer of this call
 // (mapped for the call by IpcComm::zc_*), read in place -- no staging copy. Then
 //   ALLREDUCE_2SHOT   buf[r] = rank r's tensor (in = out); bytes = whole rows of W tiles
+//   REDUCE_2SHOT      buf[r] = rank r's tensor, reduced tiles go to stg[r]; whole rows of W tiles
 //   BROADCAST_2SHOT   buf[r] = rank r's tensor;             bytes = whole rows of W tiles
 //   ALLGATHER/GATHER  buf[r] = rank r's input;              bytes = whole tiles
+//   SCATTER           buf[root] = the root's flat list, chunk q at q * zstride; whole tiles
 //   REDUCE_SCATTER    buf[r] = rank r's flat input, chunk q at q * zstride; bytes = whole tiles
 //   ALLTOALL          buf[r] = rank r's flat input, chunk q at q * zstride; bytes = whole tiles
-// and every call ends with a departure barrier (no peer reads my buffer any more
-// once my kernel is done, so the caller may overwrite or free it).
+// and every call whose last phase reads user buffers ends with a departure barrier
+// (no peer reads my buffer any more once my kernel is done, so the caller may
+// overwrite or free it).
 struct IpcCall {
   IpcColl coll;
   DType dtype;

@@ -137,7 +137,7 @@ constexpr int kCopyDepth = 4;
 // (staging is sized to whole rows, see kern::ipc_staging_bytes); valid() = 0 there.
 template <int W>
 struct OwnerRowMap {
-  const IpcView* v;
+  char* const* bufs;  // the owners' buffers (IpcView::buf, or ::stg for a zero-copy reduce)
   size_t poff;  // offset of this call in the staging buffers (0: one buffer)
   char* d;
   size_t dlim;
@@ -152,7 +152,7 @@ struct OwnerRowMap {
   __device__ const char* src(int, size_t i) const {
     int q;
     const size_t t = tile(i, q);
-    return v->buf[q] + poff + t * kTile;
+    return bufs[q] + poff + t * kTile;
   }
   __device__ char* dst(size_t i) const {
     int q;
@@ -253,6 +253,23 @@ __device__ __forceinline__ void ipc_reduce_zc(const IpcView& v, const IpcCall& c
       const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
       pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
     }
+  } else if (c.coll == IpcColl::REDUCE_2SHOT) {
+    // rooted: the owners reduce from every rank's tensor into their STAGING (non-root
+    // tensors stay untouched), the root pulls every owner's tiles from there. After the
+    // data barrier nobody reads a user tensor any more: no departure barrier (staging
+    // reuse is guarded by the next call's arrival barrier).
+    {
+      const AllSrcMap<W> m{&v, 0, v.stg[me], c.bytes, (size_t)me + W * b, W * G, nt};
+      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+    }
+    tr.mark(5);
+    block_barrier(v, ep + 2u);
+    tr.mark(6);
+    if (me == c.root) {
+      const OwnerRowMap<W> m{v.stg, 0, v.buf[me], c.bytes, (uint32_t)(me + b), b, G, nt / W};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+    }
+    return;
   } else if (c.coll == IpcColl::REDUCE_SCATTER) {
     const AllSrcMap<W> m{&v, (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
     pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
@@ -310,7 +327,7 @@ __device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall&
       if (c.coll == IpcColl::REDUCE_2SHOT && me != c.root) return;
       // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
       {
-        const OwnerRowMap<W> m{&v, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
+        const OwnerRowMap<W> m{v.buf, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
         pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;

@@ -39,8 +39,11 @@ def work(rank, size, sizes, iters):
         rs_in = torch.ones(n // size * size, device=dev)
         rs_out = torch.empty(n // size, device=dev)
         a2a_out = torch.empty_like(rs_in)
+        sc_list = list(rs_in.chunk(size)) if rank == 0 else None  # flat views: read in place
         cases = {
             "all_reduce": lambda: dist.all_reduce(x),
+            "reduce": lambda: dist.reduce(x, dst=0),
+            "scatter": lambda: dist.scatter(rs_out, scatter_list=sc_list, src=0),
             "broadcast": lambda: dist.broadcast(x, 0),
             "all_gather": lambda: dist.all_gather_into_tensor(ag_out, ag_in),
             "reduce_scatter": lambda: dist.reduce_scatter_tensor(rs_out, rs_in),
@@ -83,12 +86,13 @@ if __name__ == "__main__":
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--sizes", default="1M,4M,16M,64M,256M")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--modes", default="staged,zc", help="comma list of staged|zc (one mode per rocprof run)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     sizes = parse_sizes(a.sizes)
     runs = {}
-    for mode in ("staged", "zc"):
+    for mode in a.modes.split(","):
         env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC": "1" if mode == "zc" else "0", "PDCC_IPC_1SHOT_MAX": "256K"}
         out = launch(work, a.world, args=(sizes, a.iters), bind_device=True, timeout_s=60, env=env,
                      join_timeout_s=500)
@@ -98,6 +102,7 @@ if __name__ == "__main__":
             print(json.dumps({"world_on_one_gpu": a.world, "mode": mode, "coll": coll, "bytes": int(nb),
                               "us": round(us, 1)}), flush=True)
         print(json.dumps({"mode": mode, "correct": out[0]["correct"], "zc_calls": out[0]["zc_calls"]}), flush=True)
-    speed = {k: round(runs["staged"]["us"][k] / runs["zc"]["us"][k], 2) for k in runs["zc"]["us"]}
-    print(json.dumps({"world_on_one_gpu": a.world, "speedup_staged_over_zc": speed,
-                      "correct": runs["staged"]["correct"] and runs["zc"]["correct"]}), flush=True)
+    if len(runs) == 2:
+        speed = {k: round(runs["staged"]["us"][k] / runs["zc"]["us"][k], 2) for k in runs["zc"]["us"]}
+        print(json.dumps({"world_on_one_gpu": a.world, "speedup_staged_over_zc": speed,
+                          "correct": runs["staged"]["correct"] and runs["zc"]["correct"]}), flush=True)

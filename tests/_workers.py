@@ -881,6 +881,19 @@ def zero_copy(rank, size, device="cuda"):
         torch.zeros(size * tile * 200 + 9, device=d)
     dist.broadcast(b, src=1)
     ok["broadcast"] = bool(torch.equal(b, torch.arange(b.numel(), dtype=torch.float32, device=d)))
+    for n in (size * tile * 300, size * tile * 300 + 77):  # rooted reduce: non-roots keep their input
+        base = torch.arange(n, device=d, dtype=torch.float32) % 1000
+        t = base * (rank + 1)
+        dist.reduce(t, dst=size - 1)
+        want = base * tri if rank == size - 1 else base * (rank + 1)
+        ok[f"reduce_{n}"] = bool(torch.equal(t, want))
+    sc_n = tile * 280 + 3
+    for flat in (True, False):  # scatter from the root's list: flat views are read in place
+        pool = torch.arange(size * sc_n, dtype=torch.float32, device=d)
+        lst = list(pool.chunk(size)) if flat else [pool[q * sc_n:(q + 1) * sc_n].clone() for q in range(size)]
+        o = torch.empty(sc_n, device=d)
+        dist.scatter(o, scatter_list=lst if rank == 0 else None, src=0)
+        ok[f"scatter_flat{int(flat)}"] = bool(torch.equal(o, pool[rank * sc_n:(rank + 1) * sc_n]))
     m2 = tile * 260
     full = torch.arange(size * m2, dtype=torch.float32, device=d)
     ins = list(full.chunk(size)) if rank == 0 else [full[q * m2:(q + 1) * m2].clone() for q in range(size)]
