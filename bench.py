@@ -322,12 +322,12 @@ def run_extras(world, rank, dev, native, x):
         return f.item() > 0
 
     big = (1 << 30) if not SMALL else (64 << 20)
-    for algo in ("rccl", "ipc"):
+    for algo in ("rccl", "ipc", "ipc_push"):
         try:
             gb.set_algo(algo)
             progress(f"algo A/B: {algo}")
             for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, 256 << 20, big):
-                if nbytes == 256 << 20 and SMALL:
+                if nbytes == 256 << 20 and SMALL or (algo == "ipc_push" and nbytes < (1 << 20)):
                     continue
                 t = x[: nbytes // 4]
                 lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
@@ -340,7 +340,7 @@ def run_extras(world, rank, dev, native, x):
             # the other collectives at 1 MiB and the big size (S = total bytes, nccl-tests factors)
             from pytorch_distributed_collective_communication_amd.utils import busbw as bb
 
-            for nbytes in (1 << 20, big):
+            for nbytes in ((1 << 20, big) if algo != "ipc_push" else ()):  # push: all_reduce only
                 per = nbytes // 4 // world
                 src = x[:per]
                 full = torch.empty(per * world, device=dev)

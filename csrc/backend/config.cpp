@@ -41,6 +41,7 @@ const char* algo_name(Algo a) {
     case Algo::RCCL: return "rccl";
     case Algo::IPC: return "ipc";
     case Algo::HOST: return "host";
+    case Algo::IPC_PUSH: return "ipc_push";
   }
   return "?";
 }
@@ -53,7 +54,8 @@ Config Config::from_env() {
     else if (s == "rccl") c.force_algo = Algo::RCCL;
     else if (s == "ipc") c.force_algo = Algo::IPC;
     else if (s == "host") c.force_algo = Algo::HOST;
-    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|ipc|host, got " + s);
+    else if (s == "ipc_push") c.force_algo = Algo::IPC_PUSH;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|ipc|ipc_push|host, got " + s);
   }
   c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
   c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);
@@ -63,9 +65,10 @@ Config Config::from_env() {
   c.ipc_selftest = env_bool("PDCC_IPC_SELFTEST", c.ipc_selftest);
   c.ipc_selftest_ms = env_int("PDCC_IPC_SELFTEST_MS", c.ipc_selftest_ms);
   c.ipc_zc = env_bool("PDCC_IPC_ZC", c.ipc_zc);
+  c.ipc_push = env_bool("PDCC_IPC_PUSH", c.ipc_push);
   c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
   c.ipc_zc_cache = std::max<size_t>(1, env_size("PDCC_IPC_ZC_CACHE", c.ipc_zc_cache));
-  c.autotune =env_bool("PDCC_AUTOTUNE", c.autotune);
+  c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
   c.autotune_max = env_size("PDCC_AUTOTUNE_MAX", c.autotune_max);
   c.autotune_sample = std::max<size_t>(env_size("PDCC_AUTOTUNE_SAMPLE", c.autotune_sample), 64u << 10);
@@ -140,7 +143,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")

@@ -9,7 +9,10 @@
 
 namespace pdcc {
 
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST };
+// IPC_PUSH: the push all-reduce (zero-copy, every remote access a write), an autotuner
+// candidate next to the pull protocols of IPC
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH };
+inline bool is_ipc(Algo a) { return a == Algo::IPC || a == Algo::IPC_PUSH; }
 
 struct Config {
   // algorithm selection
@@ -25,6 +28,9 @@ struct Config {
   // a copy into the staging buffer (all-reduce: ~55% less HBM traffic per rank). Mappings are
   // cached per peer allocation (ipc_zc_cache exports per rank, LRU).
   bool ipc_zc = true;                      // PDCC_IPC_ZC
+  // The autotuner also races the push all-reduce (owners receive their tiles by remote writes,
+  // reduce locally and write the result into every rank's tensor) for zero-copy sizes.
+  bool ipc_push = true;                    // PDCC_IPC_PUSH
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
   size_t ipc_zc_cache = 16;                // PDCC_IPC_ZC_CACHE
   // Before a group first uses a device, every rank runs the IPC protocol once on known data (1-shot

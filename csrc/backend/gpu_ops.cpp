@@ -630,6 +630,8 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
     if (cfg_.force_algo == Algo::HOST) return Algo::HOST;
     if (cfg_.force_algo == Algo::RCCL && rccl_can) return Algo::RCCL;
     if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
+    if (cfg_.force_algo == Algo::IPC_PUSH && ipc_can)  // only all_reduce has a push protocol
+      return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
       if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
@@ -712,8 +714,9 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
   ok = ok && all_ok;
   ic.zc_settle(ok);
   if (!ok) return 0;
-  if (call.coll == kern::IpcColl::REDUCE_2SHOT) {
-    // the rooted reduce stages its reduced tiles: chunks of at most the staging cap
+  if (call.coll == kern::IpcColl::REDUCE_2SHOT || call.coll == kern::IpcColl::ALLREDUCE_PUSH) {
+    // the rooted reduce stages its reduced tiles, the push all-reduce receives its owned
+    // tiles in staging: chunks of at most the staging cap
     const size_t chunk = std::max(unit, ic.max_staging() / unit * unit);
     for (size_t off = 0; off < body; off += chunk) {
       kern::IpcCall c = call;
@@ -739,6 +742,7 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;
+  if (rest.coll == kern::IpcColl::ALLREDUCE_PUSH) rest.coll = kern::IpcColl::ALLREDUCE_2SHOT;  // zero-copy only
   rest.bytes = call.bytes - body;
   for (int k = 0; k < kern::kMaxRanks; ++k) {
     if (call.in[k]) rest.in[k] = static_cast<const char*>(call.in[k]) + body;
@@ -850,7 +854,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
 }
 
 // =================================================================== autotuner
-std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const {
+std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can,
+                                                      bool zc_can) const {
   std::vector<Algo> v;
   if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || !ipc_can || !same_host_ || coalescing_) return v;
   if ((int)c >= 32 || !(cfg_.autotune_colls & (1u << (int)c))) return v;
@@ -859,6 +864,10 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
   else return {};
   v.push_back(Algo::IPC);
+  // the push all-reduce (zero-copy sizes): every remote access a write instead of a read
+  if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
+      bytes > cfg_.ipc_1shot_max)
+    v.push_back(Algo::IPC_PUSH);
   return v;
 }
 
@@ -873,7 +882,7 @@ Algo ProcessGroupMI355X::tuned(const TuneKey& k) {
 // (topology, dtype/op support, the consensus table), so every rank picks the same.
 Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can,
                                 bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
-  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can);
+  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok);
   if (cands.empty()) return a0;
   const TuneKey key{(int)c, dtype, op, size_bucket(bytes)};
   const Algo t = tuned(key);
@@ -887,7 +896,7 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
   // every engine of the race exists before the clock starts (communicator setup is not timed)
   for (Algo a : cands) {
     if (a == Algo::RCCL) rccl(ds);
-    if (a == Algo::IPC) ipc(ds);
+    if (is_ipc(a)) ipc(ds);
   }
   return tune(key, cands);
 }
@@ -919,12 +928,12 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     }
   };
   bool has_ipc = false;
-  for (Algo a : cands) has_ipc = has_ipc || a == Algo::IPC;
+  for (Algo a : cands) has_ipc = has_ipc || is_ipc(a);
   Spin spin(has_ipc ? ds.ipc.get() : nullptr, (uint64_t)cfg_.autotune_spin_ms, tuning_);
   // 0) warm-up: one run each (staging growth, first-touch), then check every result
   //    against the reference engine's on identical data
   for (size_t k = 0; k < n; ++k) {
-    if (cands[k] == Algo::IPC)
+    if (is_ipc(cands[k]))
       if (const char* d = std::getenv("PDCC_TEST_AUTOTUNE_DELAY"))  // test hook "rank:ms": a late peer
         if (std::atoi(d) == rank_) {
           PDCC_HIP(hipStreamSynchronize(s));
@@ -936,7 +945,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   std::vector<double> v(2 * n, 0.0);  // [estimate_us x n, mismatch x n], MAX-reduced across ranks
   const bool ipc_fault = has_ipc && ds.ipc && ds.ipc->error_word() != 0;
   for (size_t k = 1; k < n; ++k)
-    v[n + k] = (cands[k] == Algo::IPC && ipc_fault) ? 2.0 : (same(0, k) ? 0.0 : 1.0);
+    v[n + k] = (is_ipc(cands[k]) && ipc_fault) ? 2.0 : (same(0, k) ? 0.0 : 1.0);
   {  // agree on faults first (every rank's stream is drained: no IPC kernel is running)
     std::vector<double> f(v.begin() + n, v.end());
     shm().allreduce(f.data(), f.size(), at::kDouble, RedOpType::MAX, timeout_);
@@ -994,10 +1003,11 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   TuneEntry te;
   te.ref = cands[0];
   te.iters = iters;
+  te.valid = true;
   for (size_t k = 0; k < n; ++k) {
-    if (cands[k] == Algo::IPC) {
-      te.ipc_us = med[k];
-      te.valid = v[n + k] == 0.0;
+    if (is_ipc(cands[k])) {
+      (cands[k] == Algo::IPC ? te.ipc_us : te.push_us) = med[k];
+      te.valid = te.valid && v[n + k] == 0.0;
     } else {
       te.rccl_us = med[k];  // the reference engine (RCCL, or the host transport without RCCL)
     }
@@ -1008,8 +1018,8 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     tune_[key] = te;
   }
   if (cfg_.log_level >= 1 && rank_ == 0)
-    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us%s (%d runs each) -> %s\n",
-            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.ipc_us,
+    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us, ipc_push %.1f us%s (%d runs each) -> %s\n",
+            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.ipc_us, te.push_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -1029,6 +1039,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.ref = algo_name(e.ref);
     r.rccl_us = e.rccl_us;
     r.ipc_us = e.ipc_us;
+    r.push_us = e.push_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);
     r.iters = e.iters;
@@ -1041,12 +1052,13 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
 void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko,
                                            ncclDataType_t nd, ncclRedOp_t no, bool nok, RedOpType op, int root,
                                            bool rooted, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
     const bool one_shot = w.nbytes() <= cfg_.ipc_1shot_max;
     c.coll = rooted ? (one_shot ? kern::IpcColl::REDUCE_1SHOT : kern::IpcColl::REDUCE_2SHOT)
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
+    if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     c.dtype = kd;
     c.op = ko;
     c.root = root;
@@ -1056,7 +1068,8 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     c.out[0] = w.data_ptr();
     // 2-shot reads the peers' tensors in place (all-reduce: reduced in place too;
     // rooted reduce: into staging, so non-root tensors stay untouched)
-    if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT || c.coll == kern::IpcColl::REDUCE_2SHOT)
+    if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT || c.coll == kern::IpcColl::REDUCE_2SHOT ||
+        c.coll == kern::IpcColl::ALLREDUCE_PUSH)
       ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
     else
       ipc_chunked(ic, c, ic.max_staging(), s);
@@ -1348,7 +1361,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     return cpu_done(cname, {t});
   }
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
@@ -1357,7 +1370,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  record(cname, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  record(cname, is_ipc(a) ? (one_shot ? "ipc_1shot" : a == Algo::IPC_PUSH && !rooted ? "ipc_push" : "ipc_2shot")
+                          : "rccl", bytes, t0);
   return work;
 }
 

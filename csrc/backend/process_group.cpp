@@ -669,7 +669,8 @@ void ProcessGroupMI355X::set_algo(const std::string& a) {
   else if (a == "rccl") cfg_.force_algo = Algo::RCCL;
   else if (a == "ipc") cfg_.force_algo = Algo::IPC;
   else if (a == "host") cfg_.force_algo = Algo::HOST;
-  else TORCH_CHECK(false, "set_algo: expected auto|rccl|ipc|host, got ", a);
+  else if (a == "ipc_push") cfg_.force_algo = Algo::IPC_PUSH;
+  else TORCH_CHECK(false, "set_algo: expected auto|rccl|ipc|ipc_push|host, got ", a);
 }
 
 void ProcessGroupMI355X::set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max) {

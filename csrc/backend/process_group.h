@@ -431,7 +431,8 @@ class ProcessGroupMI355X : public c10d::Backend {
     uint64_t lo, hi;  // bucket [lo, hi) in bytes (per-rank payload, see tune_bytes in gpu_ops.cpp)
     std::string ref;  // reference engine: rccl, or host where RCCL is unavailable
     double rccl_us, ipc_us;
-    bool valid;       // IPC result matched the reference engine's on every rank
+    double push_us;   // push all-reduce (0 = not raced)
+    bool valid;       // IPC result(s) matched the reference engine's on every rank
     std::string algo;
     int iters;        // timed runs per engine (median taken)
   };
@@ -445,7 +446,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
     Algo ref = Algo::RCCL;
-    double rccl_us = 0, ipc_us = 0;
+    double rccl_us = 0, ipc_us = 0, push_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
     int iters = 0;
@@ -456,7 +457,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::mutex tune_mu_;
   std::atomic<bool> tuning_{false};  // an autotune race is running: IPC spin timeouts are its verdict
   // engines worth timing for this call (reference engine first); empty = no tuning
-  std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can) const;
+  std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can, bool zc_can) const;
   Algo tuned(const TuneKey& k);
   // engine for one call: the static choice `a0`, or the tuned one for this key (tuning now,
   // through `tune(cands)`, when the key has no decision yet)

@@ -316,8 +316,11 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 size_t ipc_signal_bytes() { return (size_t)(kCountWord + kMaxBlocks) * sizeof(uint32_t); }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
-  if (c.zc)  // peers read the user buffers in place; a rooted reduce stages its reduced tiles
-    return c.coll == IpcColl::REDUCE_2SHOT ? (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes : 0;
+  if (c.zc)  // peers read the user buffers in place; a rooted reduce stages its reduced tiles,
+             // the push all-reduce receives W slots of bytes / W
+    return c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH
+               ? (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes : 0;
+  if (c.coll == IpcColl::ALLREDUCE_PUSH) return 0;  // (zero-copy only; rejected by ipc_launch)
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
   switch (c.coll) {
     case IpcColl::SCATTER:
@@ -343,7 +346,7 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   if (v.world < 2 || v.world > kMaxRanks) return hipErrorInvalidValue;
   if (c.zc) {  // in-place reads of user buffers: whole tiles (2-shot: whole rows of W tiles), no over-read
     const bool rows = c.coll == IpcColl::ALLREDUCE_2SHOT || c.coll == IpcColl::BROADCAST_2SHOT ||
-                      c.coll == IpcColl::REDUCE_2SHOT;
+                      c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH;
     const bool known = rows || c.coll == IpcColl::ALLGATHER || c.coll == IpcColl::GATHER ||
                        c.coll == IpcColl::SCATTER || c.coll == IpcColl::REDUCE_SCATTER ||
                        c.coll == IpcColl::ALLTOALL;
@@ -356,6 +359,7 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
     size_t g;
     switch (c.coll) {
       case IpcColl::ALLREDUCE_2SHOT:
+      case IpcColl::ALLREDUCE_PUSH:
       case IpcColl::REDUCE_2SHOT:
       case IpcColl::BROADCAST_2SHOT:
         g = (nt + v.world - 1) / v.world;  // rows
@@ -370,7 +374,9 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   }
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);
+  if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc) return hipErrorInvalidValue;
   const bool reducing = c.coll == IpcColl::ALLREDUCE_1SHOT || c.coll == IpcColl::ALLREDUCE_2SHOT ||
+                        c.coll == IpcColl::ALLREDUCE_PUSH ||
                         c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
                         c.coll == IpcColl::REDUCE_SCATTER;
   if (!reducing) {

@@ -174,24 +174,27 @@ struct PipeLds {
   static constexpr int kBytes = DEPTH * NSRC * kTile;
 };
 
-// Wait for tile i (< DEPTH-1) of the prologue: BASE younger loads plus the i
-// stores of the consumes issued since that tile (vmcnt needs an immediate).
-template <int BASE, int DEPTH>
+// Wait for tile i (< DEPTH-1) of the prologue: BASE younger loads plus the
+// i * ST stores of the consumes issued since that tile (vmcnt needs an immediate).
+template <int BASE, int DEPTH, int ST = 1>
 __device__ __forceinline__ void wait_prologue(int i) {
   switch (i) {
     case 0: wait_vmcnt<BASE>(); break;
-    case 1: if constexpr (DEPTH > 2) wait_vmcnt<BASE + 1>(); break;
-    case 2: if constexpr (DEPTH > 3) wait_vmcnt<BASE + 2>(); break;
-    case 3: if constexpr (DEPTH > 4) wait_vmcnt<BASE + 3>(); break;
-    case 4: if constexpr (DEPTH > 5) wait_vmcnt<BASE + 4>(); break;
-    case 5: if constexpr (DEPTH > 6) wait_vmcnt<BASE + 5>(); break;
-    default: if constexpr (DEPTH > 7) wait_vmcnt<BASE + 6>(); break;
+    case 1: if constexpr (DEPTH > 2) wait_vmcnt<BASE + 1 * ST>(); break;
+    case 2: if constexpr (DEPTH > 3) wait_vmcnt<BASE + 2 * ST>(); break;
+    case 3: if constexpr (DEPTH > 4) wait_vmcnt<BASE + 3 * ST>(); break;
+    case 4: if constexpr (DEPTH > 5) wait_vmcnt<BASE + 4 * ST>(); break;
+    case 5: if constexpr (DEPTH > 6) wait_vmcnt<BASE + 5 * ST>(); break;
+    default: if constexpr (DEPTH > 7) wait_vmcnt<BASE + 6 * ST>(); break;
   }
 }
 
-template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
+// NDST > 1: every reduced vector is stored to NDST destinations, m.dst(j, i) for
+// j < NDST (whole tiles only: the push all-reduce writes each owner's result into
+// every rank's tensor); the vmcnt accounting counts NDST stores per consume.
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int NDST = 1>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
-  static_assert((DEPTH - 1) * (NSRC + 1) < 64, "pipeline too deep for vmcnt");
+  static_assert((DEPTH - 1) * (NSRC + NDST) < 64, "pipeline too deep for vmcnt");
   static_assert(DEPTH >= 2 && DEPTH <= 8, "prologue wait counts are written out for DEPTH <= 8");
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -222,12 +225,17 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
     }
     wait_lgkm0();
     const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
-    char* d = m.dst(i);
-    const size_t lim = m.valid(i);
-    if (lane_off + 16 <= lim) {
-      *reinterpret_cast<uint4*>(d + lane_off) = r;
-    } else if (lane_off < lim) {
-      store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
+    if constexpr (NDST == 1) {
+      char* d = m.dst(i);
+      const size_t lim = m.valid(i);
+      if (lane_off + 16 <= lim) {
+        *reinterpret_cast<uint4*>(d + lane_off) = r;
+      } else if (lane_off < lim) {
+        store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NDST; ++j) *reinterpret_cast<uint4*>(m.dst(j, i) + lane_off) = r;
     }
   };
 
@@ -246,9 +254,9 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
     // in issue order, so the count must be exact (a looser one lets tile i's
     // last load still be in flight when its LDS slot is read).
     if (i >= (size_t)(DEPTH - 1)) {
-      wait_vmcnt<(DEPTH - 1) * (NSRC + 1)>();
+      wait_vmcnt<(DEPTH - 1) * (NSRC + NDST)>();
     } else {
-      wait_prologue<(DEPTH - 1) * NSRC, DEPTH>((int)i);
+      wait_prologue<(DEPTH - 1) * NSRC, DEPTH, NDST>((int)i);
     }
     consume(i, stage);
     stage = (stage + 1 == DEPTH) ? 0 : stage + 1;

@@ -112,6 +112,8 @@ enum class IpcColl : int32_t {
   REDUCE_SCATTER,        // stage W chunks, barrier, rank r reduces chunk r
   ALLTOALL,              // stage W chunks, barrier, rank r pulls chunk r of every peer
   BARRIER,               // flags only
+  ALLREDUCE_PUSH,        // zero-copy only: push tiles to their owners' staging, owners reduce and
+                         // push the result into every rank's tensor (remote writes, no remote reads)
   kCount
 };
 
@@ -121,6 +123,7 @@ enum class IpcColl : int32_t {
 // Zero-copy calls (`zc` = 1): IpcView::buf[r] is rank r's USER buffer of this call
 // (mapped for the call by IpcComm::zc_*), read in place -- no staging copy. Then
 //   ALLREDUCE_2SHOT   buf[r] = rank r's tensor (in = out); bytes = whole rows of W tiles
+//   ALLREDUCE_PUSH    buf[r] = rank r's tensor, stg[r] = its staging (W slots of bytes / W); whole rows
 //   REDUCE_2SHOT      buf[r] = rank r's tensor, reduced tiles go to stg[r]; whole rows of W tiles
 //   BROADCAST_2SHOT   buf[r] = rank r's tensor;             bytes = whole rows of W tiles
 //   ALLGATHER/GATHER  buf[r] = rank r's input;              bytes = whole tiles

@@ -192,6 +192,55 @@ struct PeerRowMap {
   __device__ size_t valid(size_t) const { return kTile; }
 };
 
+// Push all-reduce phase 1: my tile of every row that another rank q owns goes to
+// slot `me` of q's staging (slot s, row r at (s * nrows + r) * kTile). Local reads,
+// remote writes; owners rotated per item, row and block like PeerRowMap.
+template <int W>
+struct PushMap {
+  const char* mine;   // my tensor
+  char* const* stgs;  // every rank's staging (IpcView::stg)
+  int me;
+  uint32_t rot;
+  size_t first, stride, nrows;
+  __device__ size_t count() const { return first < nrows ? ((nrows - 1 - first) / stride + 1) * (W - 1) : 0; }
+  __device__ size_t row(size_t i, int& q) const {
+    const uint32_t k = (uint32_t)i / (W - 1), j = (uint32_t)i - k * (W - 1);
+    q = (me + 1 + (int)((rot + j + k) % (W - 1))) % W;
+    return first + stride * k;
+  }
+  __device__ const char* src(int, size_t i) const {
+    int q;
+    const size_t r = row(i, q);
+    return mine + ((size_t)q + (size_t)W * r) * kTile;
+  }
+  __device__ char* dst(size_t i) const {
+    int q;
+    const size_t r = row(i, q);
+    return stgs[q] + ((size_t)me * nrows + r) * kTile;
+  }
+  __device__ size_t valid(size_t) const { return kTile; }
+};
+
+// Push all-reduce phase 2: my owned tile of row r reduced from the W-1 staged
+// slots and my own tensor (sources in rank order: every rank's copy is the same
+// owner's bits), stored into every rank's tensor (destination j = rank j).
+template <int W>
+struct PushReduceMap {
+  char* const* bufs;  // every rank's tensor (IpcView::buf)
+  const char* stg;    // my staging (slot s, row r at (s * nrows + r) * kTile)
+  int me;
+  size_t first, stride, nrows;
+  __device__ size_t count() const { return first < nrows ? (nrows - 1 - first) / stride + 1 : 0; }
+  __device__ size_t row(size_t i) const { return first + stride * i; }
+  __device__ const char* src(int k, size_t i) const {
+    const size_t r = row(i);
+    const size_t slot = ((size_t)k * nrows + r) * kTile, own = ((size_t)me + (size_t)W * r) * kTile;
+    return k == me ? bufs[me] + own : stg + slot;
+  }
+  __device__ char* dst(int j, size_t i) const { return bufs[j] + ((size_t)me + (size_t)W * row(i)) * kTile; }
+  __device__ size_t valid(size_t) const { return kTile; }
+};
+
 // all-gather / gather / all-to-all: (tile t of this block, source rank q) pairs;
 // source q's tile lives at v->buf[q] + sbase + t*kTile and lands in out[q].
 template <int W>
@@ -253,6 +302,22 @@ __device__ __forceinline__ void ipc_reduce_zc(const IpcView& v, const IpcCall& c
       const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
       pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
     }
+  } else if (c.coll == IpcColl::ALLREDUCE_PUSH) {
+    // every remote access is a write (xGMI writes are posted; reads wait a round trip)
+    const size_t nrows = nt / W;
+    {  // phase 1: my tiles to their owners' staging slots
+      const PushMap<W> m{v.buf[me], v.stg, me, (uint32_t)b, b, G, nrows};
+      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+    }
+    tr.mark(5);
+    block_barrier(v, ep + 2u);
+    tr.mark(6);
+    {  // phase 2: reduce my owned tiles, store the result into every rank's tensor
+      const PushReduceMap<W> m{v.buf, v.stg[me], me, b, G, nrows};
+      pipe_run<DT, OP, W, D, PushReduceMap<W>, W>(lds, m, c.avg_div);
+    }
+    block_barrier(v, ep + 3u);  // departure with data: the peers' results are in my tensor
+    return;
   } else if (c.coll == IpcColl::REDUCE_2SHOT) {
     // rooted: the owners reduce from every rank's tensor into their STAGING (non-root
     // tensors stay untouched), the root pulls every owner's tiles from there. After the

@@ -73,6 +73,7 @@ class Config:
     ipc_copy_max: int = 1 << 20
     ipc_max_staging: int = 1 << 30
     ipc_zc: bool = True
+    ipc_push: bool = True
     ipc_zc_min: int = 1 << 20
     ipc_zc_cache: int = 16
     ipc_spin_ms: int = 600000
@@ -106,7 +107,7 @@ _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_selftest": "PDCC_IPC_SELFTEST",
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
-    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_zc_min": "PDCC_IPC_ZC_MIN",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_zc_min": "PDCC_IPC_ZC_MIN",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
@@ -137,8 +138,8 @@ def current(environ=None) -> Config:
         raw = env.get(_ENV[f.name])
         if raw not in (None, ""):
             setattr(c, f.name, _parse(f.type, raw))
-    if c.algo not in ("auto", "rccl", "ipc", "host"):
-        raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|host, got {c.algo!r}")
+    if c.algo not in ("auto", "rccl", "ipc", "ipc_push", "host"):
+        raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|ipc_push|host, got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     if c.rccl_group_comm not in ("share", "split", "init"):

@@ -11,7 +11,9 @@ serial HBM phase in front of the link-bound one.
 
     python scripts/zc_bench.py [--world 2] [--sizes 1M,4M,...]
 
-Prints one JSON line per (mode, collective, size) and a summary line.
+Modes: staged, zc (pull protocols reading the peers' tensors in place), push (the
+zero-copy push all-reduce: remote writes only). Prints one JSON line per (mode,
+collective, size) and summary lines.
 """
 import argparse
 import json
@@ -86,14 +88,16 @@ if __name__ == "__main__":
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--sizes", default="1M,4M,16M,64M,256M")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--modes", default="staged,zc", help="comma list of staged|zc (one mode per rocprof run)")
+    ap.add_argument("--modes", default="staged,zc,push", help="comma list of staged|zc|push (one mode per rocprof run)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     sizes = parse_sizes(a.sizes)
     runs = {}
     for mode in a.modes.split(","):
-        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC": "1" if mode == "zc" else "0", "PDCC_IPC_1SHOT_MAX": "256K"}
+        # push: the zero-copy push all-reduce (remote writes only); other collectives as in zc
+        env = {"PDCC_ALGO": "ipc_push" if mode == "push" else "ipc", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
+               "PDCC_IPC_1SHOT_MAX": "256K"}
         out = launch(work, a.world, args=(sizes, a.iters), bind_device=True, timeout_s=60, env=env,
                      join_timeout_s=500)
         runs[mode] = out[0]
@@ -102,7 +106,12 @@ if __name__ == "__main__":
             print(json.dumps({"world_on_one_gpu": a.world, "mode": mode, "coll": coll, "bytes": int(nb),
                               "us": round(us, 1)}), flush=True)
         print(json.dumps({"mode": mode, "correct": out[0]["correct"], "zc_calls": out[0]["zc_calls"]}), flush=True)
-    if len(runs) == 2:
+    if "staged" in runs and "zc" in runs:
         speed = {k: round(runs["staged"]["us"][k] / runs["zc"]["us"][k], 2) for k in runs["zc"]["us"]}
         print(json.dumps({"world_on_one_gpu": a.world, "speedup_staged_over_zc": speed,
                           "correct": runs["staged"]["correct"] and runs["zc"]["correct"]}), flush=True)
+    if "zc" in runs and "push" in runs:
+        speed = {k: round(runs["zc"]["us"][k] / runs["push"]["us"][k], 2) for k in runs["push"]["us"]
+                 if k.startswith("all_reduce/")}
+        print(json.dumps({"world_on_one_gpu": a.world, "all_reduce_speedup_pull_over_push": speed,
+                          "correct": runs["push"]["correct"]}), flush=True)

@@ -78,6 +78,15 @@ def test_shared_gpu_zero_copy(world, cache):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_shared_gpu_push_all_reduce(world):
+    # the push all-reduce (remote writes only) forced; other collectives take the pull protocols
+    env = {"PDCC_ALGO": "ipc_push", "PDCC_IPC_ZC_CACHE": "4", "PDCC_IPC_1SHOT_MAX": "256K",
+           "PDCC_IPC_MAX_STAGING": "2M"}
+    for ok in _gpu_launch(W.zero_copy, world, env=env):
+        assert all(ok.values()), ok
+
+
 def test_zero_copy_selftest_gate():
     # a failed zero-copy self-test leaves the staged IPC path on (and every result right)
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_SELFTEST_FAIL": "1"}
@@ -155,7 +164,7 @@ def test_autotuner_shared_gpu():
     assert los == [64 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20], res[0]["table"]
     for e in res[0]["table"]:
         assert e["coll"] == "allreduce" and e["ipc_valid"], e
-        assert e["algo"] in ("ipc", "host") and e["ref"] == "host"
+        assert e["algo"] in ("ipc", "ipc_push", "host") and e["ref"] == "host"
         assert e["dtype"] in ("Float", "BFloat16") and e["op"] == "SUM", e
         assert e["iters"] >= 3
 
@@ -174,7 +183,7 @@ def test_autotuner_every_collective_shared_gpu():
                  ("allreduce", "Int", "BAND"), ("allreduce", "Int", "BOR")]:
         assert want in rows, (want, sorted(rows))
     for e in res[0]["table"]:
-        assert e["ipc_valid"] and e["algo"] in ("ipc", "host"), e
+        assert e["ipc_valid"] and e["algo"] in ("ipc", "ipc_push", "host"), e
 
 
 def test_autotune_ipc_timeout_is_contained():
