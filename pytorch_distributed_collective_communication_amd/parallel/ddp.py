@@ -14,7 +14,11 @@ contract, MI355X-first:
   gradient is produced (``register_post_accumulate_grad_hook``), so
   communication overlaps the rest of the backward pass on the backend's
   high-priority comm stream;
-* :meth:`finish` waits, averages (one fused scale) and unpacks;
+* the average is fused into the reduction itself (``ReduceOp.AVG``: the IPC
+  kernels divide in registers, RCCL uses ``ncclAvg``) on the mi355x backend --
+  no separate pass over the buckets; other backends get SUM plus one scale;
+* :meth:`finish` waits and unpacks every GPU bucket with ONE K2 ``multi_copy``
+  launch (per-parameter copies on CPU);
 * gradient accumulation: backward passes inside ``with bucketer.no_sync():``
   only accumulate into ``.grad``; the first backward after it launches the
   reduction of the accumulated gradients. A second backward before
@@ -89,6 +93,8 @@ class GradBucketer:
             self._add_bucket(cur)
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in params]
         self._sync = True
+        self._fused_avg = average and self.world > 1 and _is_native(group, self.buckets)
+        self._op = dist.ReduceOp.AVG if self._fused_avg else dist.ReduceOp.SUM
         self._reset()
 
     @contextlib.contextmanager
@@ -126,7 +132,7 @@ class GradBucketer:
         b.flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
         b.pending -= 1
         if b.pending == 0:
-            b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            b.work = dist.all_reduce(b.flat, op=self._op, group=self.group, async_op=True)
 
     def finish(self) -> None:
         """Wait for every bucket, average, and write the result back into ``.grad``."""
@@ -137,18 +143,45 @@ class GradBucketer:
                         p.grad = torch.zeros_like(p)
                 for p, off in zip(b.params, b.offsets):
                     b.flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
-                b.work = dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                b.work = dist.all_reduce(b.flat, op=self._op, group=self.group, async_op=True)
         for b in self.buckets:
             b.work.wait()
-            if self.average and self.world > 1:
+            if self.average and self.world > 1 and not self._fused_avg:
                 b.flat.div_(self.world)
-            for p, off in zip(b.params, b.offsets):
-                p.grad.copy_(b.flat[off:off + p.numel()].view_as(p.grad))
+            _unpack(b)
         self._reset()
 
     def remove(self) -> None:
         for h in self._hooks:
             h.remove()
+
+
+def _is_native(group, buckets) -> bool:
+    """Is ``group`` served by the mi355x backend for the buckets' device (fused AVG)?"""
+    if not buckets:
+        return False
+    try:
+        from .backend import native_backend
+
+        native_backend(group, buckets[0].flat.device.type)
+        return True
+    except Exception:
+        return False
+
+
+def _unpack(b: _Bucket) -> None:
+    views = [b.flat[off:off + p.numel()] for p, off in zip(b.params, b.offsets)]
+    grads = [p.grad.reshape(-1) if p.grad.is_contiguous() else None for p in b.params]
+    if b.flat.is_cuda and all(g is not None for g in grads):
+        try:
+            from ..ops import multi_copy
+
+            multi_copy(views, grads)  # one launch for the whole bucket
+            return
+        except Exception:  # extension unavailable: plain copies below
+            pass
+    for p, v in zip(b.params, views):
+        p.grad.copy_(v.view_as(p.grad))
 
 
 def allreduce_gradients(params: Iterable[torch.nn.Parameter], group=None, average: bool = True) -> None:
