@@ -71,8 +71,10 @@ def work(rank, size, sizes, iters):
         dist.reduce_scatter_tensor(rs_out, rs_in)
         ok = ok and bool(torch.all(rs_out == size).item())
     st = be.stats()
+    # host time per call (validation, engine choice, zero-copy handle exchange, launch)
+    host_us = {k: round(v[2] / v[0] * 1e3, 1) for k, v in st.items() if k.startswith("allreduce/") and v[0]}
     return {"us": res, "correct": ok, "zc_calls": sum(v[0] for k, v in st.items() if k.endswith("_zc")),
-            "describe": be.describe()[-160:]}
+            "host_us_per_call": host_us, "describe": be.describe()[-160:]}
 
 
 def parse_sizes(s):
@@ -105,7 +107,8 @@ if __name__ == "__main__":
             coll, nb = key.split("/")
             print(json.dumps({"world_on_one_gpu": a.world, "mode": mode, "coll": coll, "bytes": int(nb),
                               "us": round(us, 1)}), flush=True)
-        print(json.dumps({"mode": mode, "correct": out[0]["correct"], "zc_calls": out[0]["zc_calls"]}), flush=True)
+        print(json.dumps({"mode": mode, "correct": out[0]["correct"], "zc_calls": out[0]["zc_calls"],
+                          "host_us_per_call": out[0]["host_us_per_call"]}), flush=True)
     if "staged" in runs and "zc" in runs:
         speed = {k: round(runs["staged"]["us"][k] / runs["zc"]["us"][k], 2) for k in runs["zc"]["us"]}
         print(json.dumps({"world_on_one_gpu": a.world, "speedup_staged_over_zc": speed,

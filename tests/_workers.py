@@ -905,3 +905,12 @@ def zero_copy(rank, size, device="cuda"):
     ok["zc_ok"] = "zc_ok=1" in be.describe()
     dist.barrier()
     return ok
+
+
+def config_probe(rank, size):
+    """The backend's own view of its configuration (C++ Config::describe) next to
+    the Python mirror's (config.current) -- both read the same PDCC_* variables."""
+    from pytorch_distributed_collective_communication_amd import config
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    return be.describe(), config.current().__dict__
