@@ -99,3 +99,13 @@ def test_p2p_pairs_distinct_gpus():
 def test_async_ordering_distinct_gpus():
     for ok in _run(W.async_ordering, 2, env={"PDCC_STREAM": "comm"}):
         assert all(ok), ok
+
+
+@pytest.mark.parametrize("algo", ["ipc", "ipc_push"])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_zero_copy_distinct_gpus(world, algo):
+    # peers read (ipc) / write (ipc_push) each other's tensors over xGMI; a small export
+    # cache forces evictions, a small staging cap forces chunked push / rooted-reduce calls
+    env = {"PDCC_ALGO": algo, "PDCC_IPC_ZC_CACHE": "4", "PDCC_IPC_1SHOT_MAX": "256K", "PDCC_IPC_MAX_STAGING": "8M"}
+    for ok in _run(W.zero_copy, world, env=env):
+        assert all(ok.values()), ok
