@@ -404,8 +404,9 @@ def _group_with_env(world, env, timeout_s=60):
 
 def rccl_tuning(world, rank, dev, x):
     """RCCL on this node's xGMI (only where ranks sit on distinct GPUs):
-    * cta_sweep: 1 GiB all_reduce busbw for RCCL channel floors (minCTAs) default/7/14/28
-      -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate;
+    * cta_sweep: 1 GiB all_reduce busbw for RCCL channel floors (minCTAs) default/28/56/112
+      -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate (the autotuner
+      races the 112-channel child communicator, PDCC_RCCL_WIDE_CTAS, for large keys);
     * list_all_gather: all_gather into separate tensors, grouped p2p straight into the
       list (zero copy) vs ring all_gather into staging + K2 unpack;
     * group_churn: new_group(range(n)) + first all_reduce, as every reference demo does."""
@@ -420,7 +421,7 @@ def rccl_tuning(world, rank, dev, x):
     res = {}
     big = x if not SMALL else x[: (64 << 20) // 4]
     sweep = {}
-    for ctas in ("default", 7, 14, 28):
+    for ctas in ("default", 28, 56, 112):
         progress(f"rccl cta sweep: {ctas}")
         env = {"PDCC_RCCL_GROUP_COMM": "init", "PDCC_ALGO": "rccl"}
         if ctas != "default":

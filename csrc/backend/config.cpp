@@ -42,6 +42,7 @@ const char* algo_name(Algo a) {
     case Algo::IPC: return "ipc";
     case Algo::HOST: return "host";
     case Algo::IPC_PUSH: return "ipc_push";
+    case Algo::RCCL_WIDE: return "rccl_wide";
   }
   return "?";
 }
@@ -55,7 +56,8 @@ Config Config::from_env() {
     else if (s == "ipc") c.force_algo = Algo::IPC;
     else if (s == "host") c.force_algo = Algo::HOST;
     else if (s == "ipc_push") c.force_algo = Algo::IPC_PUSH;
-    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|ipc|ipc_push|host, got " + s);
+    else if (s == "rccl_wide") c.force_algo = Algo::RCCL_WIDE;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|host, got " + s);
   }
   c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
   c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);
@@ -113,6 +115,8 @@ Config Config::from_env() {
   }
   c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
   c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
+  c.rccl_wide_ctas = std::max(0, env_int("PDCC_RCCL_WIDE_CTAS", c.rccl_wide_ctas));
+  c.rccl_wide_min = env_size("PDCC_RCCL_WIDE_MIN", c.rccl_wide_min);
   if (c.rccl_min_ctas > 0 && c.rccl_max_ctas > 0 && c.rccl_min_ctas > c.rccl_max_ctas)
     throw std::runtime_error("PDCC_RCCL_MIN_CTAS must not exceed PDCC_RCCL_MAX_CTAS");
   c.world1_local = env_bool("PDCC_WORLD1_LOCAL", c.world1_local);
@@ -144,7 +148,8 @@ std::string Config::describe() const {
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
     << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
-    << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas
+    << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
+    << " rccl_wide_min=" << rccl_wide_min
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
     << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes

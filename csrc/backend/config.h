@@ -10,9 +10,11 @@
 namespace pdcc {
 
 // IPC_PUSH: the push all-reduce (zero-copy, every remote access a write), an autotuner
-// candidate next to the pull protocols of IPC
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH };
+// candidate next to the pull protocols of IPC. RCCL_WIDE: RCCL on a child communicator
+// with at least rccl_wide_ctas channels, an autotuner candidate next to the default one.
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE };
 inline bool is_ipc(Algo a) { return a == Algo::IPC || a == Algo::IPC_PUSH; }
+inline bool is_rccl(Algo a) { return a == Algo::RCCL || a == Algo::RCCL_WIDE; }
 
 struct Config {
   // algorithm selection
@@ -69,6 +71,12 @@ struct Config {
   // (ncclCommInitRank); any value set goes through ncclCommInitRankConfig.
   int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
   int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
+  // Wide RCCL: a child communicator (ncclCommSplit, own resources) with at least this many
+  // channels; the autotuner races it against the default communicator for all_reduce keys
+  // from rccl_wide_min bytes, so a node whose 7 xGMI links want more channels than RCCL's
+  // topology tuner picks gets them measured, not guessed (0 = off).
+  int rccl_wide_ctas = 112;                // PDCC_RCCL_WIDE_CTAS
+  size_t rccl_wide_min = 16u << 20;        // PDCC_RCCL_WIDE_MIN
   // Groups whose member set equals a live communicator's (new_group(range(size)) in every demo
   // of the reference): share = use that communicator (RCCL runs the ops of one communicator in
   // issue order on every stream, which is the order every rank issues them in), split =

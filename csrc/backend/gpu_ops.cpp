@@ -413,6 +413,26 @@ RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
   return *ds.rccl;
 }
 
+// The wide child of the group's communicator (collective over the group: created by
+// decide() on every rank when a key races it, or by a forced PDCC_ALGO=rccl_wide).
+RcclComm& ProcessGroupMI355X::rccl_wide(DeviceState& ds) {
+  if (ds.rccl_wide) return *ds.rccl_wide;
+  RcclComm& base = rccl(ds);
+  const auto t0 = std::chrono::steady_clock::now();
+  RcclOpts o = rccl_opts();
+  o.min_ctas = std::max(cfg_.rccl_wide_ctas, 1);
+  o.max_ctas = std::max(o.max_ctas, o.min_ctas);
+  o.split_share = 0;  // its own channels and buffers
+  auto c = std::make_shared<RcclComm>(base, rank_, o);
+  c->tag = base.tag + "#wide";
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    ds.rccl_wide = c;
+  }
+  record_setup("rccl_comm/wide", t0);
+  return *ds.rccl_wide;
+}
+
 // The send/recv channel to `peer` (created on first use; its communicator is
 // built by the channel's own thread, see PairChan).
 std::shared_ptr<PairChan> ProcessGroupMI355X::pair_chan(DeviceState& ds, int peer) {
@@ -629,6 +649,8 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
   const Algo a = [&] {
     if (cfg_.force_algo == Algo::HOST) return Algo::HOST;
     if (cfg_.force_algo == Algo::RCCL && rccl_can) return Algo::RCCL;
+    if (cfg_.force_algo == Algo::RCCL_WIDE && rccl_can)  // only all_reduce races the wide communicator
+      return c == Coll::ALLREDUCE ? Algo::RCCL_WIDE : Algo::RCCL;
     if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_PUSH && ipc_can)  // only all_reduce has a push protocol
       return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
@@ -863,6 +885,9 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
   else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
   else return {};
+  // RCCL with more channels than its topology tuner picks (large all_reduce keys)
+  if (c == Coll::ALLREDUCE && rccl_can && cfg_.rccl_wide_ctas > 0 && bytes >= cfg_.rccl_wide_min)
+    v.push_back(Algo::RCCL_WIDE);
   v.push_back(Algo::IPC);
   // the push all-reduce (zero-copy sizes): every remote access a write instead of a read
   if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
@@ -896,6 +921,7 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
   // every engine of the race exists before the clock starts (communicator setup is not timed)
   for (Algo a : cands) {
     if (a == Algo::RCCL) rccl(ds);
+    if (a == Algo::RCCL_WIDE) rccl_wide(ds);
     if (is_ipc(a)) ipc(ds);
   }
   return tune(key, cands);
@@ -1008,6 +1034,9 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     if (is_ipc(cands[k])) {
       (cands[k] == Algo::IPC ? te.ipc_us : te.push_us) = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
+    } else if (cands[k] == Algo::RCCL_WIDE) {
+      te.wide_us = med[k];
+      te.valid = te.valid && v[n + k] == 0.0;
     } else {
       te.rccl_us = med[k];  // the reference engine (RCCL, or the host transport without RCCL)
     }
@@ -1018,8 +1047,10 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     tune_[key] = te;
   }
   if (cfg_.log_level >= 1 && rank_ == 0)
-    fprintf(stderr, "[pdcc r0] autotune %s %zu B: %s %.1f us, ipc %.1f us, ipc_push %.1f us%s (%d runs each) -> %s\n",
-            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.ipc_us, te.push_us,
+    fprintf(stderr,
+            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_push %.1f us%s (%d runs each)"
+            " -> %s\n",
+            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us, te.push_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -1040,6 +1071,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.rccl_us = e.rccl_us;
     r.ipc_us = e.ipc_us;
     r.push_us = e.push_us;
+    r.wide_us = e.wide_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);
     r.iters = e.iters;
@@ -1073,9 +1105,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
       ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
     else
       ipc_chunked(ic, c, ic.max_staging(), s);
-  } else if (a == Algo::RCCL) {
+  } else if (is_rccl(a)) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
-    RcclComm& rc = rccl(ds);
+    RcclComm& rc = a == Algo::RCCL_WIDE ? rccl_wide(ds) : rccl(ds);
     if (rooted) PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
     else PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
   } else {  // HOST, synchronous
@@ -1371,7 +1403,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
   record(cname, is_ipc(a) ? (one_shot ? "ipc_1shot" : a == Algo::IPC_PUSH && !rooted ? "ipc_push" : "ipc_2shot")
-                          : "rccl", bytes, t0);
+                          : a == Algo::RCCL_WIDE ? "rccl_wide" : "rccl", bytes, t0);
   return work;
 }
 

@@ -407,6 +407,7 @@ ProcessGroupMI355X::~ProcessGroupMI355X() {
     DeviceState& ds = *kv.second;
     if (!health_->poisoned.load()) continue;
     if (ds.rccl) ds.rccl->abort();
+    if (ds.rccl_wide) ds.rccl_wide->abort();
     for (auto& p : ds.pairs) {
       std::lock_guard<std::mutex> lk(p.second->mu);
       if (p.second->comm) p.second->comm->abort();
@@ -609,6 +610,7 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
     for (auto& kv : devs_) {
       DeviceState& ds = *kv.second;
       if (ds.rccl) ds.rccl->abort();
+      if (ds.rccl_wide) ds.rccl_wide->abort();
       for (auto& p : ds.pairs) {
         std::lock_guard<std::mutex> plk(p.second->mu);
         if (p.second->comm) p.second->comm->abort();
@@ -670,7 +672,8 @@ void ProcessGroupMI355X::set_algo(const std::string& a) {
   else if (a == "ipc") cfg_.force_algo = Algo::IPC;
   else if (a == "host") cfg_.force_algo = Algo::HOST;
   else if (a == "ipc_push") cfg_.force_algo = Algo::IPC_PUSH;
-  else TORCH_CHECK(false, "set_algo: expected auto|rccl|ipc|ipc_push|host, got ", a);
+  else if (a == "rccl_wide") cfg_.force_algo = Algo::RCCL_WIDE;
+  else TORCH_CHECK(false, "set_algo: expected auto|rccl|rccl_wide|ipc|ipc_push|host, got ", a);
 }
 
 void ProcessGroupMI355X::set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max) {
@@ -733,6 +736,7 @@ void ProcessGroupMI355X::watchdog_loop() {
       DeviceState& ds = *kv.second;
       std::vector<std::shared_ptr<RcclComm>> comms;
       if (ds.rccl) comms.push_back(ds.rccl);
+      if (ds.rccl_wide) comms.push_back(ds.rccl_wide);
       for (auto& p : ds.pairs) {
         std::lock_guard<std::mutex> plk(p.second->mu);
         if (p.second->comm) comms.push_back(p.second->comm);

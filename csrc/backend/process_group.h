@@ -194,6 +194,7 @@ struct DeviceState {
   bool zc_ok = false;                   // zero-copy IPC (user buffers read in place) passed its self-test
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
+  std::shared_ptr<RcclComm> rccl_wide;  // lazy child of `rccl` with at least PDCC_RCCL_WIDE_CTAS channels
   std::shared_ptr<IpcComm> ipc;         // lazy
   std::map<int, std::shared_ptr<PairChan>> pairs;  // send/recv channels to peers on other GPUs
   std::map<int, bool> pair_distinct;               // peer on another device (RCCL-capable pair)?
@@ -307,6 +308,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   DeviceState& dev_state(const at::Tensor& t);
   void init_topology(DeviceState& ds);
   RcclComm& rccl(DeviceState& ds);
+  RcclComm& rccl_wide(DeviceState& ds);
   std::shared_ptr<PairChan> pair_chan(DeviceState& ds, int peer);
   static void pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store, std::string key,
                            int prank, int dev, int pi);
@@ -432,6 +434,7 @@ class ProcessGroupMI355X : public c10d::Backend {
     std::string ref;  // reference engine: rccl, or host where RCCL is unavailable
     double rccl_us, ipc_us;
     double push_us;   // push all-reduce (0 = not raced)
+    double wide_us;   // RCCL on the wide child communicator (0 = not raced)
     bool valid;       // IPC result(s) matched the reference engine's on every rank
     std::string algo;
     int iters;        // timed runs per engine (median taken)
@@ -446,7 +449,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
     Algo ref = Algo::RCCL;
-    double rccl_us = 0, ipc_us = 0, push_us = 0;
+    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
     int iters = 0;

@@ -125,6 +125,7 @@ PYBIND11_MODULE(_C, m) {
                d["ref_us"] = r.rccl_us;
                d["ipc_us"] = r.ipc_us;
                d["push_us"] = r.push_us;
+               d["wide_us"] = r.wide_us;
                d["ipc_valid"] = r.valid;
                d["algo"] = r.algo;
                d["iters"] = r.iters;

@@ -85,6 +85,8 @@ class Config:
     autotune_spin_ms: int = 10000
     rccl_min_ctas: int = -1
     rccl_max_ctas: int = -1
+    rccl_wide_ctas: int = 112
+    rccl_wide_min: int = 16 << 20
     rccl_group_comm: str = "share"
     rccl_split_share: bool = True
     list_gather: str = "p2p"
@@ -115,6 +117,7 @@ _ENV = {
     "rccl_group_comm": "PDCC_RCCL_GROUP_COMM", "rccl_split_share": "PDCC_RCCL_SPLIT_SHARE",
     "list_gather": "PDCC_LIST_GATHER", "eager_init": "PDCC_EAGER_INIT",
     "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",
+    "rccl_wide_ctas": "PDCC_RCCL_WIDE_CTAS", "rccl_wide_min": "PDCC_RCCL_WIDE_MIN",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
     "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
     "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",
@@ -138,8 +141,8 @@ def current(environ=None) -> Config:
         raw = env.get(_ENV[f.name])
         if raw not in (None, ""):
             setattr(c, f.name, _parse(f.type, raw))
-    if c.algo not in ("auto", "rccl", "ipc", "ipc_push", "host"):
-        raise ValueError(f"PDCC_ALGO must be auto|rccl|ipc|ipc_push|host, got {c.algo!r}")
+    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "host"):
+        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|host, got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     if c.rccl_group_comm not in ("share", "split", "init"):

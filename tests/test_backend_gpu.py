@@ -33,6 +33,13 @@ def test_world1_rccl_bulk_paths():
     assert all(res[0].values()), res[0]
 
 
+def test_world1_rccl_wide_communicator():
+    # the autotuner's wide-RCCL candidate (a split child with >= 112 channels) forced on a 1-rank communicator
+    env = {"PDCC_WORLD1_LOCAL": "0", "PDCC_ALGO": "rccl_wide"}
+    res = _gpu_launch(W.large, 1, env=env)
+    assert all(res[0].values()), res[0]
+
+
 def test_world1_rccl_with_cta_config():
     # ncclCommInitRankConfig path (channel bounds) on a 1-rank communicator
     env = {"PDCC_WORLD1_LOCAL": "0", "PDCC_RCCL_MIN_CTAS": "8", "PDCC_RCCL_MAX_CTAS": "32"}

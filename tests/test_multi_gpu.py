@@ -71,7 +71,7 @@ def test_autotuner_distinct_gpus():
         if e["op"] in ("BAND", "BOR"):  # no RCCL op: the host transport is the reference engine
             assert e["ref"] == "host" and e["algo"] in ("host", "ipc"), e
         else:
-            assert e["ref"] == "rccl" and e["algo"] in ("rccl", "ipc"), e
+            assert e["ref"] == "rccl" and e["algo"] in ("rccl", "rccl_wide", "ipc", "ipc_push"), e
 
 
 @pytest.mark.parametrize("mode", ["share", "split"])
