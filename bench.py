@@ -310,6 +310,7 @@ def run_extras(world, rank, dev, native, x):
     del a, b, c
     if world == 1:
         return out
+    out["links"] = link_summary(world)
 
     # algorithm A/B on a short-timeout subgroup (a stuck peer aborts in 60 s, not 10 min)
     g = dist.new_group(list(range(world)), timeout=datetime.timedelta(seconds=60))
@@ -382,6 +383,23 @@ def run_extras(world, rank, dev, native, x):
         except Exception as e:
             out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
     return out
+
+
+def link_summary(world):
+    """How the ranks' GPUs (cuda:0..world-1, one per rank) are connected, as the HIP
+    runtime reports it: counts of (link type, hops) over the ordered pairs, e.g.
+    {"xgmi/1": 56} for a fully connected 8-GPU xGMI node."""
+    import pytorch_distributed_collective_communication_amd as pdcc
+
+    counts: dict = {}
+    try:
+        for e in pdcc._load_native().device_links():
+            if e["src"] < world and e["dst"] < world:
+                k = f"{e['link']}/{e.get('hops', '?')}" + ("" if e.get("p2p", 1) else "/no_p2p")
+                counts[k] = counts.get(k, 0) + 1
+    except Exception as e:  # informational only
+        return {"error": f"{type(e).__name__}: {e}"[:200]}
+    return counts
 
 
 def _group_with_env(world, env, timeout_s=60):

@@ -88,6 +88,41 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
   TORCH_CHECK(e == hipSuccess, "multi_copy launch failed: ", hipGetErrorString(e));
 }
 
+// Peer links between every pair of visible GPUs, as the runtime reports them: HSA link
+// type (xGMI on an MI355X node, PCIe otherwise), hop count, P2P access / atomics and
+// the runtime's relative performance rank. Local queries only (no collective).
+py::list device_links() {
+  static const char* kLink[] = {"hypertransport", "qpi", "pcie", "infiniband", "xgmi"};
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  py::list out;
+  for (int a = 0; a < n; ++a)
+    for (int b = 0; b < n; ++b) {
+      if (a == b) continue;
+      py::dict d;
+      d["src"] = a;
+      d["dst"] = b;
+      uint32_t type = 0, hops = 0;
+      if (hipExtGetLinkTypeAndHopCount(a, b, &type, &hops) == hipSuccess) {
+        d["link"] = type < 5 ? std::string(kLink[type]) : std::to_string(type);
+        d["hops"] = hops;
+      } else {
+        (void)hipGetLastError();
+        d["link"] = "unknown";
+      }
+      int v = 0;
+      if (hipDeviceGetP2PAttribute(&v, hipDevP2PAttrAccessSupported, a, b) == hipSuccess) d["p2p"] = v;
+      if (hipDeviceGetP2PAttribute(&v, hipDevP2PAttrNativeAtomicSupported, a, b) == hipSuccess) d["atomics"] = v;
+      if (hipDeviceGetP2PAttribute(&v, hipDevP2PAttrPerformanceRank, a, b) == hipSuccess) d["perf_rank"] = v;
+      (void)hipGetLastError();
+      out.append(d);
+    }
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -168,6 +203,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
         "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);
+  m.def("device_links", &device_links,
+        "peer links between every pair of visible GPUs: link type (xgmi/pcie), hops, p2p, atomics, perf_rank");
   m.def("forwarded_rccl_env", &pdcc::forward_rccl_env,
         "NCCL_* variables set from PDCC_RCCL_* before the first communicator (once per process)");
   m.attr("MAX_RANKS_IPC") = pdcc::kern::kMaxRanks;

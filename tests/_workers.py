@@ -914,3 +914,71 @@ def config_probe(rank, size):
     from pytorch_distributed_collective_communication_amd.parallel import backend as be
 
     return be.describe(), config.current().__dict__
+
+
+def _make_opt(name):
+    import torch
+
+    return (torch.optim.SGD, {"lr": 0.05, "momentum": 0.9}) if name == "sgd" else (torch.optim.AdamW, {"lr": 1e-2})
+
+
+def zero_train(rank, size, optim="adam", steps=5, device="cpu", dtype="float32", resume=False):
+    """ZeRO-style sharded DP (parallel.zero.ShardedOptimizer) on the MLP; returns
+    (final flat params, sharded state bytes, resumed params or None). With
+    resume=True the optimizer is checkpointed after 3 steps, 2 more steps run,
+    and a fresh model + optimizer restored from the checkpoint must reproduce them."""
+    import torch
+
+    from pytorch_distributed_collective_communication_amd.models import MLP, synthetic_batch
+    from pytorch_distributed_collective_communication_amd.parallel.zero import ShardedOptimizer
+
+    d = _dev(device)
+    dt = getattr(torch, dtype)
+    cls, kw = _make_opt(optim)
+    x, y = synthetic_batch(64, device=d)
+    shard = 64 // size
+    xs, ys = x[rank * shard:(rank + 1) * shard].to(dt), y[rank * shard:(rank + 1) * shard].to(dt)
+
+    def build():
+        torch.manual_seed(100 + rank)  # different init per rank: the broadcast must fix it
+        m = MLP().to(d, dt)
+        return m, ShardedOptimizer(m.parameters(), cls, **kw)
+
+    def run(model, opt, n):
+        for _ in range(n):
+            torch.nn.functional.mse_loss(model(xs), ys).backward()
+            opt.step()
+            opt.zero_grad()
+
+    def flat(model):
+        return torch.cat([p.detach().float().reshape(-1).cpu() for p in model.parameters()]).tolist()
+
+    model, opt = build()
+    if not resume:
+        run(model, opt, steps)
+        return flat(model), opt.sharded_state_bytes(), None
+    run(model, opt, 3)
+    ck = opt.state_dict()
+    run(model, opt, 2)
+    m2, o2 = build()
+    o2.load_state_dict(ck)
+    run(m2, o2, 2)
+    return flat(model), opt.sharded_state_bytes(), flat(m2)
+
+
+def zero_reference(optim="adam", steps=5):
+    """Single process, full batch, same optimizer: what sharded DP must reproduce."""
+    import torch
+
+    from pytorch_distributed_collective_communication_amd.models import MLP, synthetic_batch
+
+    cls, kw = _make_opt(optim)
+    torch.manual_seed(100)
+    model = MLP()
+    x, y = synthetic_batch(64)
+    opt = cls(model.parameters(), **kw)
+    for _ in range(steps):
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(x), y).backward()
+        opt.step()
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()])

@@ -266,3 +266,14 @@ def test_gpu_peer_death_is_detected():
     assert "IPC" in msg or "error state" in msg or "timed out" in msg, msg
     assert elapsed < 30, elapsed
     assert ps[1].exitcode == 13
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_sharded_optimizer_on_shared_gpu(dtype):
+    # ZeRO-style step on GPU tensors: reduce_scatter(AVG) + all_gather_into_tensor via the IPC kernels
+    res = _gpu_launch(W.zero_train, 2, args=("adam", 5, "cuda", dtype))
+    ref = W.zero_reference("adam")
+    for params, _, _ in res:
+        assert params == res[0][0]
+        tol = 1e-4 if dtype == "float32" else 5e-2
+        torch.testing.assert_close(torch.tensor(params), ref, rtol=tol, atol=tol)
