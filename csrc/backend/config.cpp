@@ -98,6 +98,7 @@ Config Config::from_env() {
     }
   }
   c.ipc_spin_ms = (int64_t)env_size("PDCC_IPC_SPIN_MS", (size_t)c.ipc_spin_ms);
+  c.ipc_grid = std::min(1024, std::max(1, env_int("PDCC_IPC_GRID", c.ipc_grid)));
   c.autotune_spin_ms = (int64_t)env_size("PDCC_AUTOTUNE_SPIN_MS", (size_t)c.autotune_spin_ms);
   if (const char* gc = env("PDCC_RCCL_GROUP_COMM")) {
     std::string v(gc);
@@ -147,7 +148,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")

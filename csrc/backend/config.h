@@ -44,6 +44,10 @@ struct Config {
   // Upper bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if
   // shorter); the watchdog's abort stops a spin at once.
   int64_t ipc_spin_ms = 600000;            // PDCC_IPC_SPIN_MS
+  // Workgroup cap of the IPC kernels on distinct devices (1..1024; one workgroup pulls one
+  // row of W tiles / one tile at a time, so more workgroups = more remote reads in flight
+  // per xGMI link). Ranks sharing one device are capped at 256 / W for co-residency.
+  int ipc_grid = 512;                      // PDCC_IPC_GRID
   // Online autotuner (GPU all_reduce, groups where both RCCL and IPC are feasible): the first call
   // in each power-of-two size bucket >= autotune_min runs both engines on scratch copies, checks
   // that the IPC result matches RCCL's, times both and adopts the faster one on every rank.

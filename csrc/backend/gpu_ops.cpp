@@ -469,6 +469,7 @@ IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
     const uint64_t spin = (uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count()));
     auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging, spin,
                                        ds.shared_device, cfg_.ipc_zc_cache);
+    c->set_grid_max(cfg_.ipc_grid);
     std::lock_guard<std::mutex> lk(init_mu_);
     ds.ipc = c;
   }

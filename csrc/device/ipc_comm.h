@@ -47,6 +47,8 @@ class IpcComm {
 
   // spin timeout of the cross-GPU barriers of later launches
   void set_timeout_ms(uint64_t ms) { timeout_ticks_ = ms * 100000ull; }
+  // workgroup cap of every launch on distinct devices (PDCC_IPC_GRID); same on every rank
+  void set_grid_max(int g) { grid_max_ = g; }
   uint64_t timeout_ms() const { return timeout_ticks_ / 100000ull; }
   // a launch was captured into a graph: sequence numbers live on the device from now on
   bool graph_mode() const { return graph_mode_; }
@@ -132,6 +134,7 @@ class IpcComm {
   size_t max_staging_;
   uint64_t timeout_ticks_;
   bool shared_device_;
+  int grid_max_ = 0;  // 0: the kernel library's default cap
 
   uint32_t* my_flags_ = nullptr;          // uncached device memory
   std::vector<uint32_t*> peer_flags_;     // mapped (own entry = my_flags_)

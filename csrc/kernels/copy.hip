@@ -370,7 +370,7 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
       default:
         g = nt;
     }
-    grid = (int)std::max<size_t>(1, std::min<size_t>(g, 512));
+    grid = (int)std::max<size_t>(1, std::min<size_t>(g, c.grid_cap > 0 ? (size_t)c.grid_cap : 512));
   }
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);

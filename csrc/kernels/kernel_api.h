@@ -140,7 +140,7 @@ struct IpcCall {
   int root;
   int avg_div;
   int grid;                      // 0 = pick
-  int grid_cap;                  // > 0: upper bound on the picked grid (co-residency on shared devices)
+  int grid_cap;                  // > 0: upper bound on the picked grid (PDCC_IPC_GRID; 256/W on shared devices)
   int zc;                        // 1 = zero-copy call (see above)
   size_t bytes;                  // payload bytes (per rank / per chunk, see above)
   size_t zstride;                // zero-copy chunked inputs: byte distance between chunks
