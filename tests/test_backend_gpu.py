@@ -273,7 +273,7 @@ def test_sharded_optimizer_on_shared_gpu(dtype):
     # ZeRO-style step on GPU tensors: reduce_scatter(AVG) + all_gather_into_tensor via the IPC kernels
     res = _gpu_launch(W.zero_train, 2, args=("adam", 5, "cuda", dtype))
     ref = W.zero_reference("adam")
-    for params, _, _ in res:
-        assert params == res[0][0]
+    for params, _, _, overlapped in res:
+        assert params == res[0][0] and overlapped == 1
         tol = 1e-4 if dtype == "float32" else 5e-2
         torch.testing.assert_close(torch.tensor(params), ref, rtol=tol, atol=tol)

@@ -83,22 +83,33 @@ def test_sharded_optimizer_matches_single_process(world, optim):
     # ZeRO-style: reduce-scatter(AVG) of flat grads, sharded step, all-gather of params
     res = launch(W.zero_train, world, args=(optim,))
     ref = W.zero_reference(optim)
-    for params, state_bytes, _ in res:
+    for params, state_bytes, _, overlapped in res:
         torch.testing.assert_close(torch.tensor(params), torch.tensor(res[0][0]), rtol=0, atol=0)
         torch.testing.assert_close(torch.tensor(params), ref, rtol=1e-5, atol=1e-6)
         # each rank holds 1/world of the fp32 master weights + optimizer state (<= 3 words
         # per parameter), up to the 64-element padding of its shard
         assert state_bytes <= 12 * (ref.numel() / world + 64) + 16, state_bytes
+        assert overlapped == 1  # the single bucket's reduce-scatter started inside backward
 
 
 def test_sharded_optimizer_checkpoint_resume():
-    for params, _, resumed in launch(W.zero_train, 3, args=("adam", 5, "cpu", "float32", True)):
+    for params, _, resumed, _ in launch(W.zero_train, 3, args=("adam", 5, "cpu", "float32", True)):
         torch.testing.assert_close(torch.tensor(resumed), torch.tensor(params), rtol=0, atol=0)
 
 
 def test_sharded_optimizer_bf16_params_fp32_master():
     res = launch(W.zero_train, 2, args=("adam", 5, "cpu", "bfloat16"))
     ref = W.zero_reference("adam")
-    for params, _, _ in res:
+    for params, _, _, _ in res:
         assert params == res[0][0]  # replicas identical (the gathered bf16 shards)
         torch.testing.assert_close(torch.tensor(params), ref, rtol=5e-2, atol=5e-2)
+
+
+def test_sharded_optimizer_buckets_overlap_and_no_sync():
+    # 2 KiB buckets (several per model, each reduce-scattered during backward) and
+    # gradient accumulation over 2 micro-batches (the first under no_sync())
+    res = launch(W.zero_train, 2, args=("sgd", 5, "cpu", "float32", False, 2048, 2))
+    ref = W.zero_reference("sgd")
+    for params, _, _, overlapped in res:
+        torch.testing.assert_close(torch.tensor(params), ref, rtol=1e-5, atol=1e-6)
+        assert overlapped >= 5, overlapped
