@@ -382,6 +382,10 @@ def run_extras(world, rank, dev, native, x):
             out["rccl_tuning"] = rccl_tuning(world, rank, dev, x)
         except Exception as e:
             out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
+        try:
+            out["ipc_grid_sweep_allreduce_busbw"] = ipc_grid_sweep(world, rank, dev, x)
+        except Exception as e:
+            out["ipc_grid_sweep_error"] = f"{type(e).__name__}: {e}"[:300]
     return out
 
 
@@ -425,7 +429,6 @@ def rccl_tuning(world, rank, dev, x):
     * cta_sweep: 1 GiB all_reduce busbw for RCCL channel floors (minCTAs) default/28/56/112
       -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate (the autotuner
       races the 112-channel child communicator, PDCC_RCCL_WIDE_CTAS, for large keys);
-    * ipc_grid_sweep: the same for the IPC pull / push kernels' workgroup cap (PDCC_IPC_GRID);
     * list_all_gather: all_gather into separate tensors, grouped p2p straight into the
       list (zero copy) vs ring all_gather into staging + K2 unpack;
     * group_churn: new_group(range(n)) + first all_reduce, as every reference demo does."""
@@ -450,22 +453,6 @@ def rccl_tuning(world, rank, dev, x):
         sweep[str(ctas)] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
         dist.destroy_process_group(g)
     res["cta_sweep_allreduce_busbw"] = sweep
-    # IPC kernels' workgroup cap (PDCC_IPC_GRID): more workgroups = more remote reads /
-    # writes in flight per xGMI link; pull (ipc) and push protocols, 1 GiB all_reduce
-    gsweep = {}
-    for algo in ("ipc", "ipc_push"):
-        for grid in (256, 512, 1024):
-            progress(f"ipc grid sweep: {algo} {grid}")
-            g = _group_with_env(world, {"PDCC_ALGO": algo, "PDCC_IPC_GRID": grid})
-            t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
-            gsweep[f"{algo}_g{grid}"] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
-            dist.destroy_process_group(g)
-    v = torch.full((1 << 22,), float(rank + 1), device=dev)
-    g = _group_with_env(world, {"PDCC_ALGO": "ipc", "PDCC_IPC_GRID": 1024})
-    dist.all_reduce(v, group=g)
-    gsweep["correct_g1024"] = bool(torch.all(v == world * (world + 1) / 2).item())
-    dist.destroy_process_group(g)
-    res["ipc_grid_sweep_allreduce_busbw"] = gsweep
     per = ((256 << 20) if not SMALL else (16 << 20)) // 4
     src = torch.full((per,), float(rank), device=dev)
     for mode in ("p2p", "staged"):
@@ -490,6 +477,32 @@ def rccl_tuning(world, rank, dev, x):
         churn.append(round((time.perf_counter() - t0) * 1e3, 2))
     res["group_churn_ms"] = churn
     return res
+
+
+def ipc_grid_sweep(world, rank, dev, x):
+    """1 GiB all_reduce busbw of the IPC pull (ipc) and push protocols for workgroup caps
+    256/512/1024 (PDCC_IPC_GRID): more workgroups = more remote reads / writes in flight
+    per xGMI link. (Ranks sharing a GPU are capped at 256 / W whatever the knob says.)"""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.utils import busbw as bb
+
+    big = x if not SMALL else x[: (64 << 20) // 4]
+    gsweep = {}
+    for algo in ("ipc", "ipc_push"):
+        for grid in (256, 512, 1024):
+            progress(f"ipc grid sweep: {algo} {grid}")
+            g = _group_with_env(world, {"PDCC_ALGO": algo, "PDCC_IPC_GRID": grid})
+            t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
+            gsweep[f"{algo}_g{grid}"] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
+            dist.destroy_process_group(g)
+    v = torch.full((1 << 22,), float(rank + 1), device=dev)
+    g = _group_with_env(world, {"PDCC_ALGO": "ipc", "PDCC_IPC_GRID": 1024})
+    dist.all_reduce(v, group=g)
+    gsweep["correct_g1024"] = bool(torch.all(v == world * (world + 1) / 2).item())
+    dist.destroy_process_group(g)
+    return gsweep
 
 
 def graph_replay(world, rank, dev, n_ops=16, numel=1024):

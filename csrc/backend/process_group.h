@@ -221,6 +221,14 @@ class ProcessGroupMI355X : public c10d::Backend {
   c10::intrusive_ptr<c10d::Work> endCoalescing() override;
   void setSequenceNumberForGroup() override {}
   uint64_t getSequenceNumberForGroup() override { return op_seq_.load(); }
+  // init_process_group(device_id=...) / new_group(device_id=...): torch asks only backends
+  // that report splitting support to connect eagerly. Communicators of same-member groups
+  // are shared or ncclCommSplit from each other inside rccl(), among the members only, so
+  // the no-color split torch requests from non-members (perform_nocolor_split) is a no-op.
+  bool supportsSplitting() const override { return true; }
+  void eagerConnectSingleDevice(at::Device device) override {
+    if (device.is_cuda() && device.has_index()) eager_init(device.index());
+  }
 
   c10::intrusive_ptr<c10d::Work> broadcast(std::vector<at::Tensor>& tensors,
                                            const c10d::BroadcastOptions& opts = c10d::BroadcastOptions()) override;

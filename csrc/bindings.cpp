@@ -196,7 +196,10 @@ PYBIND11_MODULE(_C, m) {
            "PDCC_IPC_TRACE records: [seq, t_entry, t_seq, t_staged, t_barrier0, t_phase1, t_barrier1, t_exit] "
            "in 100 MHz device ticks, block 0 of each IPC kernel")
       .def("eager_init", &pdcc::ProcessGroupMI355X::eager_init, py::arg("device"),
-           py::call_guard<py::gil_scoped_release>());
+           py::call_guard<py::gil_scoped_release>())
+      // torch calls this on non-member ranks of a new group when the default group is bound
+      // to a device (see supportsSplitting in process_group.h): nothing to do here
+      .def("perform_nocolor_split", [](pdcc::ProcessGroupMI355X&, const at::Device&) {});
 
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
         py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");

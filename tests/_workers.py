@@ -992,3 +992,32 @@ def zero_reference(optim="adam", steps=5):
         torch.nn.functional.mse_loss(model(x), y).backward()
         opt.step()
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+def device_id_probe(rank, size, path, device="cuda"):
+    """init_process_group(device_id=...) connects eagerly (torch calls
+    eagerConnectSingleDevice on backends that report splitting support); a subgroup
+    that leaves the last rank out makes torch ask that rank for a no-color split
+    (perform_nocolor_split, a no-op here). Re-initialises the world on a FileStore."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    dist.destroy_process_group()
+    d = _dev(device)
+    dist.init_process_group("mi355x", init_method="file://" + path, rank=rank, world_size=size, device_id=d)
+    b = be.native_backend(None, "cuda")
+    out = {"splitting": b.supports_splitting, "desc": b.describe(),
+           "before": sorted(k for k in b.stats() if k.startswith("rccl_comm/"))}
+    members = list(range(max(1, size - 1)))
+    sub = dist.new_group(members)
+    x = torch.full((4096,), float(rank + 1), device=d)
+    dist.all_reduce(x)
+    ok = bool(torch.all(x == size * (size + 1) / 2))
+    if rank in members:
+        y = torch.full((4096,), float(rank + 1), device=d)
+        dist.all_reduce(y, group=sub)
+        ok = ok and bool(torch.all(y == len(members) * (len(members) + 1) / 2))
+    out["ok"] = ok
+    return out

@@ -277,3 +277,17 @@ def test_sharded_optimizer_on_shared_gpu(dtype):
         assert params == res[0][0] and overlapped == 1
         tol = 1e-4 if dtype == "float32" else 5e-2
         torch.testing.assert_close(torch.tensor(params), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_init_with_device_id_connects_eagerly(world, tmp_path):
+    # torch's eager-init contract (init_process_group(device_id=...)): the communicator
+    # (world 1, RCCL) / the topology + IPC mappings (2 ranks sharing the GPU) exist
+    # before the first collective; a subgroup without the last rank still works
+    res = _gpu_launch(W.device_id_probe, world, args=(str(tmp_path / "store"),), env={"PDCC_WORLD1_LOCAL": "0"})
+    for r in res:
+        assert r["ok"] and r["splitting"], r
+        if world == 1:
+            assert r["before"] == ["rccl_comm/init"], r
+        else:
+            assert "ipc_ok=1" in r["desc"] and "ipc=1" in r["desc"], r
