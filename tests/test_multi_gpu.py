@@ -109,3 +109,21 @@ def test_zero_copy_distinct_gpus(world, algo):
     env = {"PDCC_ALGO": algo, "PDCC_IPC_ZC_CACHE": "4", "PDCC_IPC_1SHOT_MAX": "256K", "PDCC_IPC_MAX_STAGING": "8M"}
     for ok in _run(W.zero_copy, world, env=env):
         assert all(ok.values()), ok
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_optimizer_distinct_gpus(world):
+    # ZeRO-style step: bucket reduce-scatters (AVG) launched during backward, all-gather of params
+    res = _run(W.zero_train, world, args=("adam", 5, "cuda", "float32", False, 4096))
+    ref = W.zero_reference("adam")
+    for params, _, _, overlapped in res:
+        assert params == res[0][0] and overlapped >= 2
+        torch.testing.assert_close(torch.tensor(params), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_init_with_device_id_distinct_gpus(world, tmp_path):
+    # eager RCCL communicator at init_process_group(device_id=...); the last rank is a
+    # non-member of a subgroup (torch asks it for a no-color split)
+    for r in _run(W.device_id_probe, world, args=(str(tmp_path / "store"),)):
+        assert r["ok"] and r["before"] == ["rccl_comm/init"], r
