@@ -1021,3 +1021,25 @@ def device_id_probe(rank, size, path, device="cuda"):
         ok = ok and bool(torch.all(y == len(members) * (len(members) + 1) / 2))
     out["ok"] = ok
     return out
+
+
+def object_collectives(rank, size, device="cpu"):
+    """torch's pickled-object collectives (all_gather_object, broadcast_object_list,
+    gather_object, scatter_object_list) run on top of our all_gather/broadcast/
+    gather/scatter with variable-size uint8 payloads."""
+    import torch.distributed as dist
+
+    out = {}
+    objs = [None] * size
+    dist.all_gather_object(objs, {"r": rank, "s": "x" * (rank * 1000)})
+    out["all_gather_object"] = [(o["r"], len(o["s"])) for o in objs]
+    lst = [{"a": 1}, list(range(5000))] if rank == 0 else [None, None]
+    dist.broadcast_object_list(lst, src=0)
+    out["broadcast_object_list"] = [lst[0], len(lst[1])]
+    g = [None] * size if rank == 0 else None
+    dist.gather_object(("g", rank), g, dst=0)
+    out["gather_object"] = g
+    so = [None]
+    dist.scatter_object_list(so, [("s", i) for i in range(size)] if rank == 0 else None, src=0)
+    out["scatter_object_list"] = so[0]
+    return out

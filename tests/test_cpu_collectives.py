@@ -115,3 +115,12 @@ def test_p2p_between_two_ranks_of_a_larger_group(world):
 def test_abort_and_shutdown_hooks():
     for ok in launch(W.lifecycle_probe, 2, args=("cpu",), timeout_s=60, join_timeout_s=120):
         assert all(ok.values()), ok
+
+
+def test_object_collectives():
+    res = launch(W.object_collectives, 3)
+    for r, got in enumerate(res):
+        assert got["all_gather_object"] == [(q, q * 1000) for q in range(3)]
+        assert got["broadcast_object_list"] == [{"a": 1}, 5000]
+        assert got["gather_object"] == ([("g", q) for q in range(3)] if r == 0 else None)
+        assert got["scatter_object_list"] == ("s", r)
