@@ -43,6 +43,7 @@ const char* algo_name(Algo a) {
     case Algo::HOST: return "host";
     case Algo::IPC_PUSH: return "ipc_push";
     case Algo::RCCL_WIDE: return "rccl_wide";
+    case Algo::IPC_WIDE: return "ipc_wide";
   }
   return "?";
 }
@@ -57,7 +58,8 @@ Config Config::from_env() {
     else if (s == "host") c.force_algo = Algo::HOST;
     else if (s == "ipc_push") c.force_algo = Algo::IPC_PUSH;
     else if (s == "rccl_wide") c.force_algo = Algo::RCCL_WIDE;
-    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|host, got " + s);
+    else if (s == "ipc_wide") c.force_algo = Algo::IPC_WIDE;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|host, got " + s);
   }
   c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
   c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);
@@ -99,6 +101,7 @@ Config Config::from_env() {
   }
   c.ipc_spin_ms = (int64_t)env_size("PDCC_IPC_SPIN_MS", (size_t)c.ipc_spin_ms);
   c.ipc_grid = std::min(1024, std::max(1, env_int("PDCC_IPC_GRID", c.ipc_grid)));
+  c.ipc_wide_grid = std::min(1024, std::max(0, env_int("PDCC_IPC_WIDE_GRID", c.ipc_wide_grid)));
   c.autotune_spin_ms = (int64_t)env_size("PDCC_AUTOTUNE_SPIN_MS", (size_t)c.autotune_spin_ms);
   if (const char* gc = env("PDCC_RCCL_GROUP_COMM")) {
     std::string v(gc);
@@ -148,7 +151,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")

@@ -12,8 +12,10 @@ namespace pdcc {
 // IPC_PUSH: the push all-reduce (zero-copy, every remote access a write), an autotuner
 // candidate next to the pull protocols of IPC. RCCL_WIDE: RCCL on a child communicator
 // with at least rccl_wide_ctas channels, an autotuner candidate next to the default one.
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE };
-inline bool is_ipc(Algo a) { return a == Algo::IPC || a == Algo::IPC_PUSH; }
+// IPC_WIDE: the pull all-reduce with ipc_wide_grid workgroups (more remote reads in flight
+// per xGMI link), an autotuner candidate next to IPC for bulk all_reduce keys.
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE };
+inline bool is_ipc(Algo a) { return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE; }
 inline bool is_rccl(Algo a) { return a == Algo::RCCL || a == Algo::RCCL_WIDE; }
 
 struct Config {
@@ -48,6 +50,9 @@ struct Config {
   // row of W tiles / one tile at a time, so more workgroups = more remote reads in flight
   // per xGMI link). Ranks sharing one device are capped at 256 / W for co-residency.
   int ipc_grid = 512;                      // PDCC_IPC_GRID
+  // Workgroup cap of the IPC_WIDE autotuner candidate (all_reduce keys >= rccl_wide_min on
+  // distinct GPUs); raced only when larger than ipc_grid (0 = off).
+  int ipc_wide_grid = 1024;                // PDCC_IPC_WIDE_GRID
   // Online autotuner (GPU all_reduce, groups where both RCCL and IPC are feasible): the first call
   // in each power-of-two size bucket >= autotune_min runs both engines on scratch copies, checks
   // that the IPC result matches RCCL's, times both and adopts the faster one on every rank.

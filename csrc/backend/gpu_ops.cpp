@@ -655,6 +655,8 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
     if (cfg_.force_algo == Algo::IPC && ipc_can) return Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_PUSH && ipc_can)  // only all_reduce has a push protocol
       return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
+    if (cfg_.force_algo == Algo::IPC_WIDE && ipc_can)  // only all_reduce races the wide grid
+      return c == Coll::ALLREDUCE ? Algo::IPC_WIDE : Algo::IPC;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
       if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
@@ -890,6 +892,10 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   if (c == Coll::ALLREDUCE && rccl_can && cfg_.rccl_wide_ctas > 0 && bytes >= cfg_.rccl_wide_min)
     v.push_back(Algo::RCCL_WIDE);
   v.push_back(Algo::IPC);
+  // the pull all-reduce with more workgroups (distinct GPUs: rccl_can; shared devices are
+  // capped for co-residency anyway)
+  if (c == Coll::ALLREDUCE && rccl_can && cfg_.ipc_wide_grid > cfg_.ipc_grid && bytes >= cfg_.rccl_wide_min)
+    v.push_back(Algo::IPC_WIDE);
   // the push all-reduce (zero-copy sizes): every remote access a write instead of a read
   if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
       bytes > cfg_.ipc_1shot_max)
@@ -1033,7 +1039,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   te.valid = true;
   for (size_t k = 0; k < n; ++k) {
     if (is_ipc(cands[k])) {
-      (cands[k] == Algo::IPC ? te.ipc_us : te.push_us) = med[k];
+      (cands[k] == Algo::IPC ? te.ipc_us : cands[k] == Algo::IPC_WIDE ? te.ipc_wide_us : te.push_us) = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
     } else if (cands[k] == Algo::RCCL_WIDE) {
       te.wide_us = med[k];
@@ -1049,9 +1055,10 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   }
   if (cfg_.log_level >= 1 && rank_ == 0)
     fprintf(stderr,
-            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_push %.1f us%s (%d runs each)"
-            " -> %s\n",
-            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us, te.push_us,
+            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us%s"
+            " (%d runs each) -> %s\n",
+            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us,
+            te.ipc_wide_us, te.push_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -1072,6 +1079,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.rccl_us = e.rccl_us;
     r.ipc_us = e.ipc_us;
     r.push_us = e.push_us;
+    r.ipc_wide_us = e.ipc_wide_us;
     r.wide_us = e.wide_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);
@@ -1092,6 +1100,7 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     c.coll = rooted ? (one_shot ? kern::IpcColl::REDUCE_1SHOT : kern::IpcColl::REDUCE_2SHOT)
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
+    if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
     c.dtype = kd;
     c.op = ko;
     c.root = root;
@@ -1403,7 +1412,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  record(cname, is_ipc(a) ? (one_shot ? "ipc_1shot" : a == Algo::IPC_PUSH && !rooted ? "ipc_push" : "ipc_2shot")
+  record(cname, is_ipc(a) ? (one_shot                           ? "ipc_1shot"
+                             : a == Algo::IPC_PUSH && !rooted ? "ipc_push"
+                             : a == Algo::IPC_WIDE            ? "ipc_2shot_wide"
+                                                              : "ipc_2shot")
                           : a == Algo::RCCL_WIDE ? "rccl_wide" : "rccl", bytes, t0);
   return work;
 }

@@ -443,6 +443,7 @@ class ProcessGroupMI355X : public c10d::Backend {
     double rccl_us, ipc_us;
     double push_us;   // push all-reduce (0 = not raced)
     double wide_us;   // RCCL on the wide child communicator (0 = not raced)
+    double ipc_wide_us;  // pull all-reduce with ipc_wide_grid workgroups (0 = not raced)
     bool valid;       // IPC result(s) matched the reference engine's on every rank
     std::string algo;
     int iters;        // timed runs per engine (median taken)
@@ -457,7 +458,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
     Algo ref = Algo::RCCL;
-    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0;
+    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0, ipc_wide_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
     int iters = 0;

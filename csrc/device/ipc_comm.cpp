@@ -292,7 +292,7 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
     // all ranks' grids must be co-resident on ONE device (test setups): stay well
     // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
     call.grid_cap = std::max(1, 256 / world_);
-  } else if (grid_max_ > 0) {
+  } else if (grid_max_ > 0 && call.grid_cap <= 0) {  // (a call may carry its own cap: IPC_WIDE)
     call.grid_cap = grid_max_;
   }
   DeviceScope ds(device_);

@@ -6,7 +6,7 @@ group is constructed; :func:`current` shows what a new group would use and
 
 | variable | default | meaning |
 |---|---|---|
-| PDCC_ALGO | auto | force ``rccl`` / ``ipc`` / ``host`` for GPU tensors (preferred if feasible) |
+| PDCC_ALGO | auto | force ``rccl`` / ``rccl_wide`` / ``ipc`` / ``ipc_push`` / ``ipc_wide`` / ``host`` for GPU tensors (preferred if feasible) |
 | PDCC_IPC | 1 | enable the hipIpc peer-memory path |
 | PDCC_IPC_SELFTEST | 1 | run the IPC protocol once on known data when a group first uses a GPU; any failure on any rank disables IPC for that group |
 | PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers (capped by the group timeout) |
@@ -17,6 +17,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_MAX_STAGING | 1G | staging bytes; larger calls are chunked |
 | PDCC_IPC_SPIN_MS | 600000 | bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if shorter) |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
+| PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
 | PDCC_AUTOTUNE_SAMPLE | 1G | bytes per engine the tuning runs move (a prefix of the caller's data) |
@@ -79,6 +80,7 @@ class Config:
     ipc_zc_cache: int = 16
     ipc_spin_ms: int = 600000
     ipc_grid: int = 512
+    ipc_wide_grid: int = 1024
     autotune: bool = True
     autotune_min: int = 64 << 10
     autotune_max: int = 1 << 42
@@ -114,7 +116,7 @@ _ENV = {
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_zc_min": "PDCC_IPC_ZC_MIN",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
-    "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
+    "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",
     "rccl_group_comm": "PDCC_RCCL_GROUP_COMM", "rccl_split_share": "PDCC_RCCL_SPLIT_SHARE",
     "list_gather": "PDCC_LIST_GATHER", "eager_init": "PDCC_EAGER_INIT",
@@ -143,8 +145,8 @@ def current(environ=None) -> Config:
         raw = env.get(_ENV[f.name])
         if raw not in (None, ""):
             setattr(c, f.name, _parse(f.type, raw))
-    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "host"):
-        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|host, got {c.algo!r}")
+    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "ipc_wide", "host"):
+        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|host, got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     if c.rccl_group_comm not in ("share", "split", "init"):

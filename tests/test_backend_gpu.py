@@ -94,6 +94,14 @@ def test_shared_gpu_push_all_reduce(world):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("grid", ["64", "1024"])
+def test_shared_gpu_wide_grid_all_reduce(grid):
+    # the ipc_wide all-reduce (its own workgroup cap per call) forced, and the group-wide cap
+    env = {"PDCC_ALGO": "ipc_wide", "PDCC_IPC_GRID": grid, "PDCC_IPC_1SHOT_MAX": "256K"}
+    for ok in _gpu_launch(W.zero_copy, 2, env=env):
+        assert all(ok.values()), ok
+
+
 def test_zero_copy_selftest_gate():
     # a failed zero-copy self-test leaves the staged IPC path on (and every result right)
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_SELFTEST_FAIL": "1"}

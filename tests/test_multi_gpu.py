@@ -71,7 +71,7 @@ def test_autotuner_distinct_gpus():
         if e["op"] in ("BAND", "BOR"):  # no RCCL op: the host transport is the reference engine
             assert e["ref"] == "host" and e["algo"] in ("host", "ipc"), e
         else:
-            assert e["ref"] == "rccl" and e["algo"] in ("rccl", "rccl_wide", "ipc", "ipc_push"), e
+            assert e["ref"] == "rccl" and e["algo"] in ("rccl", "rccl_wide", "ipc", "ipc_wide", "ipc_push"), e
 
 
 @pytest.mark.parametrize("mode", ["share", "split"])
@@ -101,7 +101,7 @@ def test_async_ordering_distinct_gpus():
         assert all(ok), ok
 
 
-@pytest.mark.parametrize("algo", ["ipc", "ipc_push"])
+@pytest.mark.parametrize("algo", ["ipc", "ipc_push", "ipc_wide"])
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_zero_copy_distinct_gpus(world, algo):
     # peers read (ipc) / write (ipc_push) each other's tensors over xGMI; a small export
