@@ -666,6 +666,22 @@ c10d::ErrorType ProcessGroupMI355X::getError() {
   return c10d::ErrorType::COMM_ERROR;
 }
 
+c10::intrusive_ptr<c10d::Backend> ProcessGroupMI355X::split(const c10::intrusive_ptr<c10d::Store>& store,
+                                                            const std::vector<int>& ranks,
+                                                            const c10::intrusive_ptr<c10d::Backend::Options>& opts) {
+  const auto me = std::find(ranks.begin(), ranks.end(), rank_);
+  if (me == ranks.end()) return nullptr;  // not a member of this split
+  std::vector<int64_t> global;
+  for (int r : ranks) {
+    TORCH_CHECK(r >= 0 && r < size_, "ProcessGroupMI355X::split: rank ", r, " is not in this group");
+    global.push_back(global_ranks_.empty() ? r : global_ranks_[r]);
+  }
+  const auto timeout = opts ? opts->timeout : timeout_;
+  std::string name = opts && !opts->group_name.empty() ? opts->group_name : group_name_ + ":split";
+  return c10::make_intrusive<ProcessGroupMI355X>(store, (int)(me - ranks.begin()), (int)ranks.size(), timeout,
+                                                 std::move(global), std::move(name));
+}
+
 void ProcessGroupMI355X::set_algo(const std::string& a) {
   if (a == "auto") cfg_.force_algo = Algo::AUTO;
   else if (a == "rccl") cfg_.force_algo = Algo::RCCL;

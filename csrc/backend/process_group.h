@@ -229,6 +229,11 @@ class ProcessGroupMI355X : public c10d::Backend {
   void eagerConnectSingleDevice(at::Device device) override {
     if (device.is_cuda() && device.has_index()) eager_init(device.index());
   }
+  // dist.split_group: a new backend over `ranks` (this group's ranks, sorted) on the split's
+  // store; its communicators come up lazily like any group's (same-member sharing applies)
+  c10::intrusive_ptr<c10d::Backend> split(const c10::intrusive_ptr<c10d::Store>& store,
+                                          const std::vector<int>& ranks,
+                                          const c10::intrusive_ptr<c10d::Backend::Options>& opts) override;
 
   c10::intrusive_ptr<c10d::Work> broadcast(std::vector<at::Tensor>& tensors,
                                            const c10d::BroadcastOptions& opts = c10d::BroadcastOptions()) override;

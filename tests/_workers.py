@@ -1043,3 +1043,28 @@ def object_collectives(rank, size, device="cpu"):
     dist.scatter_object_list(so, [("s", i) for i in range(size)] if rank == 0 else None, src=0)
     out["scatter_object_list"] = so[0]
     return out
+
+
+def split_probe(rank, size, path, device="cuda"):
+    """dist.split_group (ProcessGroup::splitGroup -> our Backend::split; torch needs
+    the world bound to a device, so it is re-initialised with device_id on a
+    FileStore): disjoint halves, an all_reduce and a broadcast inside each, then
+    one on the world."""
+    import torch
+    import torch.distributed as dist
+
+    dist.destroy_process_group()
+    d = _dev(device)
+    dist.init_process_group("mi355x", init_method="file://" + path, rank=rank, world_size=size, device_id=d)
+    half = size // 2
+    parts = [list(range(half)), list(range(half, size))]
+    g = dist.split_group(split_ranks=parts)
+    mine = parts[0] if rank < half else parts[1]
+    x = torch.full((1000,), float(rank + 1), device=d)
+    dist.all_reduce(x, group=g)
+    y = torch.full((10,), float(rank), device=d)
+    dist.broadcast(y, src=mine[0], group=g)
+    z = torch.ones(3, device=d)
+    dist.all_reduce(z)
+    return {"sum": x[0].item(), "want": float(sum(r + 1 for r in mine)), "bcast": y[0].item(), "root": mine[0],
+            "world": z[0].item(), "grank": dist.get_rank(g), "gsize": dist.get_world_size(g)}

@@ -299,3 +299,10 @@ def test_init_with_device_id_connects_eagerly(world, tmp_path):
             assert r["before"] == ["rccl_comm/init"], r
         else:
             assert "ipc_ok=1" in r["desc"] and "ipc=1" in r["desc"], r
+
+
+def test_split_group_on_shared_gpu(tmp_path):
+    # dist.split_group -> Backend::split: two halves of a 4-rank world on one GPU (IPC inside each)
+    for r, got in enumerate(_gpu_launch(W.split_probe, 4, args=(str(tmp_path / "store"),))):
+        assert got["sum"] == got["want"] and got["bcast"] == got["root"] and got["world"] == 4.0, got
+        assert got["grank"] == r % 2 and got["gsize"] == 2, got

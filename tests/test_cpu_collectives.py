@@ -124,3 +124,4 @@ def test_object_collectives():
         assert got["broadcast_object_list"] == [{"a": 1}, 5000]
         assert got["gather_object"] == ([("g", q) for q in range(3)] if r == 0 else None)
         assert got["scatter_object_list"] == ("s", r)
+

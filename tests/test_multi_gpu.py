@@ -127,3 +127,10 @@ def test_init_with_device_id_distinct_gpus(world, tmp_path):
     # non-member of a subgroup (torch asks it for a no-color split)
     for r in _run(W.device_id_probe, world, args=(str(tmp_path / "store"),)):
         assert r["ok"] and r["before"] == ["rccl_comm/init"], r
+
+
+def test_split_group_distinct_gpus(tmp_path):
+    # dist.split_group -> Backend::split: halves of a 4-GPU world, RCCL / IPC inside each
+    for r, got in enumerate(_run(W.split_probe, 4, args=(str(tmp_path / "store"),))):
+        assert got["sum"] == got["want"] and got["bcast"] == got["root"] and got["world"] == 4.0, got
+        assert got["grank"] == r % 2 and got["gsize"] == 2, got
