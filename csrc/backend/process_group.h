@@ -281,6 +281,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   void abort() override;
   void shutdown() override;
   void setTimeout(std::chrono::milliseconds timeout) override { timeout_ = timeout; }
+  int64_t timeout_ms() const { return timeout_.count(); }
   c10d::ErrorType getError() override;
 
   // ---- extras exposed to Python

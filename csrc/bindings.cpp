@@ -186,6 +186,7 @@ PYBIND11_MODULE(_C, m) {
       .def("flight_recorder_dump", &pdcc::ProcessGroupMI355X::flight_recorder_dump, py::arg("last") = 16)
       .def("reset_stats", &pdcc::ProcessGroupMI355X::reset_stats)
       .def("describe", &pdcc::ProcessGroupMI355X::describe)
+      .def("timeout_ms", &pdcc::ProcessGroupMI355X::timeout_ms)
       .def("last_algo", &pdcc::ProcessGroupMI355X::last_algo)
       .def("healthy", &pdcc::ProcessGroupMI355X::healthy)
       .def("health_message", &pdcc::ProcessGroupMI355X::health_message)

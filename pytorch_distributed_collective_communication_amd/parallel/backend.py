@@ -29,7 +29,34 @@ _orig_init = None
 def _native():
     from .. import _load_native
 
-    return _load_native()
+    C = _load_native()
+    if not hasattr(C.ProcessGroupMI355X, "options"):
+        C.ProcessGroupMI355X.options = property(_backend_options)
+    return C
+
+
+_options_cls = None
+
+
+def _backend_options(backend):
+    """``backend.options`` (torch's split_group deep-copies the parent's): a c10d
+    Backend.Options carrying this group's timeout, deep-copyable."""
+    global _options_cls
+    import datetime
+
+    import torch
+
+    if _options_cls is None:
+        base = torch._C._distributed_c10d.Backend.Options
+
+        class _Options(base):
+            def __deepcopy__(self, memo):
+                o = _Options(self.backend, self._timeout)
+                o.group_name = self.group_name
+                return o
+
+        _options_cls = _Options
+    return _options_cls(BACKEND_NAME, datetime.timedelta(milliseconds=backend.timeout_ms()))
 
 
 def _create(dist_opts, backend_opts):
