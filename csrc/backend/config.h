@@ -36,6 +36,10 @@ struct Config {
   // reduce locally and write the result into every rank's tensor) for zero-copy sizes.
   bool ipc_push = true;                    // PDCC_IPC_PUSH
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
+  // All-reduces up to this size (<= 64 KiB, kern::kLLMaxBytes) use the LL protocol: every
+  // rank pushes flag-tagged 8-byte words into its peers' signal areas and polls its own --
+  // no staging copy and no barrier (0 = off; gated by its own self-test).
+  size_t ipc_ll_max = 64u << 10;           // PDCC_IPC_LL_MAX
   size_t ipc_zc_cache = 16;                // PDCC_IPC_ZC_CACHE
   // Before a group first uses a device, every rank runs the IPC protocol once on known data (1-shot
   // and 2-shot all-reduce, all-gather) with a short spin timeout and checks the results; one failure

@@ -347,18 +347,22 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
   } else if (!cfg_.ipc_selftest) {
     ds.ipc_ok = true;
     ds.zc_ok = cfg_.ipc_zc;
+    ds.ll_ok = cfg_.ipc_ll_max > 0;
   } else if (all_cached) {
     ds.ipc_ok = cached != '0';  // an earlier group with these members tested this topology
-    ds.zc_ok = cached == '2';
+    ds.zc_ok = ((cached - '0') & 2) != 0;
+    ds.ll_ok = ((cached - '0') & 4) != 0;
   } else {
     ds.ipc_ok = ipc_selftest(ds);
     std::lock_guard<std::mutex> lk(g_verdict_mu);
-    g_ipc_verdict[vkey] = !ds.ipc_ok ? '0' : ds.zc_ok ? '2' : '1';
+    // bit 0: IPC, bit 1: zero-copy, bit 2: LL all-reduce
+    g_ipc_verdict[vkey] = !ds.ipc_ok ? '0' : (char)('1' + (ds.zc_ok ? 2 : 0) + (ds.ll_ok ? 4 : 0));
   }
   ds.topo = true;
   if (cfg_.log_level >= 1)
-    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d zc_ok=%d shared_device=%d%s\n", rank_, d, bus,
-            (int)ds.rccl_ok, (int)ds.ipc_ok, (int)ds.zc_ok, (int)shared, all_cached ? " (cached IPC verdict)" : "");
+    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d zc_ok=%d ll_ok=%d shared_device=%d%s\n", rank_, d,
+            bus, (int)ds.rccl_ok, (int)ds.ipc_ok, (int)ds.zc_ok, (int)ds.ll_ok, (int)shared,
+            all_cached ? " (cached IPC verdict)" : "");
 }
 
 RcclOpts ProcessGroupMI355X::rccl_opts() const {
@@ -641,6 +645,58 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
     if (!ds.zc_ok)
       fprintf(stderr, "[pdcc r%d] zero-copy IPC self-test failed (%s): group '%s' stages every IPC call\n", rank_,
               zok ? "on another rank" : zwhy.c_str(), group_name_.c_str());
+  }
+  // LL all-reduce: payloads with a partial last line and the largest one, each twice
+  // (both slot parities), bf16 and f32
+  ds.ll_ok = false;
+  if (cfg_.ipc_ll_max > 0) {
+    bool lok = true;
+    std::string lwhy;
+    IpcComm& ic = *ds.ipc;
+    try {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
+      const hipStream_t s = ds.stream.stream();
+      const double tri = size_ * (size_ + 1) / 2.0;
+      const int64_t full = (int64_t)(kern::kLLMaxBytes / 4);
+      for (const int64_t n : {int64_t{1}, int64_t{1001}, full, full}) {
+        for (const auto dt : {at::kFloat, at::kBFloat16}) {
+          const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(dt);
+          const int64_t ne = dt == at::kFloat ? n : std::max<int64_t>(1, n / 2 - 1);  // bf16: odd byte counts too
+          const at::Tensor base = at::arange(ne, opt).remainder(3);
+          at::Tensor x = base + (double)(rank_ + 1);
+          kern::IpcCall c{};
+          c.coll = kern::IpcColl::ALLREDUCE_LL;
+          c.dtype = dt == at::kFloat ? kern::DType::F32 : kern::DType::BF16;
+          c.op = kern::RedOp::SUM;
+          c.avg_div = size_;
+          c.bytes = x.nbytes();
+          c.in[0] = x.data_ptr();
+          c.out[0] = x.data_ptr();
+          ic.launch(c, s);
+          lok = at::equal(x, base * (double)size_ + tri) && lok;
+        }
+      }
+      PDCC_HIP(hipStreamSynchronize(s));
+      if (ic.error_word() != 0) {
+        lok = false;
+        lwhy = "an LL poll timed out";
+        ic.clear_error();
+      } else if (!lok) {
+        lwhy = "wrong data";
+      }
+    } catch (const std::exception& e) {
+      lok = false;
+      lwhy = e.what();
+    }
+    if (const char* f = std::getenv("PDCC_IPC_LL_SELFTEST_FAIL"))  // test hook: this rank reports a failure
+      if (*f && std::atoi(f) == rank_) {
+        lok = false;
+        lwhy = "PDCC_IPC_LL_SELFTEST_FAIL";
+      }
+    ds.ll_ok = vote("pdcc/ipc_selftest/ll", lok);
+    if (!ds.ll_ok)
+      fprintf(stderr, "[pdcc r%d] LL all-reduce self-test failed (%s): group '%s' uses the 1-shot protocol\n", rank_,
+              lok ? "on another rank" : lwhy.c_str(), group_name_.c_str());
   }
   ds.ipc->set_timeout_ms((uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count())));
   return true;
@@ -1101,6 +1157,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
+    // small all-reduce: flag-tagged pushes, no staging copy, no barrier
+    if (!rooted && ds.ll_ok && w.nbytes() <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes))
+      c.coll = kern::IpcColl::ALLREDUCE_LL;
     c.dtype = kd;
     c.op = ko;
     c.root = root;
@@ -1412,7 +1471,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  record(cname, is_ipc(a) ? (one_shot                           ? "ipc_1shot"
+  const bool ll = !rooted && ds.ll_ok && bytes <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes);
+  record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
+                             : one_shot                         ? "ipc_1shot"
                              : a == Algo::IPC_PUSH && !rooted ? "ipc_push"
                              : a == Algo::IPC_WIDE            ? "ipc_2shot_wide"
                                                               : "ipc_2shot")

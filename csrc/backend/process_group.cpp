@@ -595,7 +595,7 @@ std::string ProcessGroupMI355X::describe() {
   std::lock_guard<std::mutex> lk(init_mu_);
   for (auto& kv : devs_)
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
-      << ", zc_ok=" << kv.second->zc_ok << ", shared_device=" << kv.second->shared_device
+      << ", zc_ok=" << kv.second->zc_ok << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
       << ", rccl=" << (kv.second->rccl != nullptr) << ", ipc=" << (kv.second->ipc != nullptr)
       << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0) << "}";

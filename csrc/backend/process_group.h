@@ -192,6 +192,7 @@ struct DeviceState {
   bool rccl_ok = false;                 // all ranks on distinct devices
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
   bool zc_ok = false;                   // zero-copy IPC (user buffers read in place) passed its self-test
+  bool ll_ok = false;                   // LL all-reduce (flag-tagged pushes, no barrier) passed its self-test
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
   std::shared_ptr<RcclComm> rccl_wide;  // lazy child of `rccl` with at least PDCC_RCCL_WIDE_CTAS channels

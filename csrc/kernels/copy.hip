@@ -312,8 +312,8 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
   return hipSuccess;
 }
 
-// block-pairwise flags, then the per-block call counters
-size_t ipc_signal_bytes() { return (size_t)(kCountWord + kMaxBlocks) * sizeof(uint32_t); }
+// block-pairwise flags, the per-block call counters, the LL control words and LL slots
+size_t ipc_signal_bytes() { return kLLOffset + 2 * (size_t)kMaxRanks * kLLSlotBytes; }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
   if (c.zc)  // peers read the user buffers in place; a rooted reduce stages its reduced tiles,
@@ -321,6 +321,7 @@ size_t ipc_staging_bytes(const IpcCall& c, int world) {
     return c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH
                ? (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes : 0;
   if (c.coll == IpcColl::ALLREDUCE_PUSH) return 0;  // (zero-copy only; rejected by ipc_launch)
+  if (c.coll == IpcColl::ALLREDUCE_LL) return 0;    // words go straight into the peers' LL slots
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
   switch (c.coll) {
     case IpcColl::SCATTER:
@@ -367,6 +368,9 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
       case IpcColl::BARRIER:
         g = 1;
         break;
+      case IpcColl::ALLREDUCE_LL:
+        g = ((c.bytes + 7) / 8 + kBlockThreads - 1) / kBlockThreads;  // one 8-byte line per thread
+        break;
       default:
         g = nt;
     }
@@ -375,8 +379,9 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);
   if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc) return hipErrorInvalidValue;
+  if (c.coll == IpcColl::ALLREDUCE_LL && (c.zc || c.bytes == 0 || c.bytes > kLLMaxBytes)) return hipErrorInvalidValue;
   const bool reducing = c.coll == IpcColl::ALLREDUCE_1SHOT || c.coll == IpcColl::ALLREDUCE_2SHOT ||
-                        c.coll == IpcColl::ALLREDUCE_PUSH ||
+                        c.coll == IpcColl::ALLREDUCE_PUSH || c.coll == IpcColl::ALLREDUCE_LL ||
                         c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
                         c.coll == IpcColl::REDUCE_SCATTER;
   if (!reducing) {

@@ -79,6 +79,18 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 // replays (which repeat kernel arguments verbatim) run the same code.
 constexpr int kCountWord = kMaxBlocks * kMaxRanks;  // u32 index of counters[0] in the signal area
 constexpr int kEpochsPerCall = 4;                   // arrival, data, second data phase (+1 spare)
+
+// LL ("low-latency") all-reduce for small payloads (IpcColl::ALLREDUCE_LL): every 8-byte
+// word a rank pushes carries 4 data bytes and the call's epoch, so a receiver polls the
+// data itself -- no staging copy, no barrier. Receive slots live in the (uncached)
+// signal area after the flags and counters: [parity][source rank] slots of kLLSlotBytes.
+// The epoch is per rank and per LL call: read by every block at entry, advanced by the
+// block that finishes last (ctl[0] = epoch of the last finished call, ctl[1] = exit count).
+constexpr int kLLCtlWord = kCountWord + kMaxBlocks;        // u32 index of ctl[0] in the signal area
+constexpr size_t kLLOffset = 40960;                        // byte offset of the receive slots
+constexpr size_t kLLMaxBytes = 64u << 10;                  // payload per rank of one LL call
+constexpr size_t kLLSlotBytes = 2 * kLLMaxBytes;           // 8-byte words of 4 data bytes
+static_assert(kLLOffset >= (size_t)(kLLCtlWord + 16) * 4, "LL slots overlap the signal words");
 struct IpcView {
   char* buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes; zero-copy: user buffers
   char* stg[kMaxRanks];        // staging buffer per rank (zero-copy calls that still stage results)
@@ -114,6 +126,7 @@ enum class IpcColl : int32_t {
   BARRIER,               // flags only
   ALLREDUCE_PUSH,        // zero-copy only: push tiles to their owners' staging, owners reduce and
                          // push the result into every rank's tensor (remote writes, no remote reads)
+  ALLREDUCE_LL,          // <= kLLMaxBytes: push flag-tagged words into every peer's LL slot, poll, reduce
   kCount
 };
 

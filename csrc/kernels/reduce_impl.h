@@ -421,6 +421,100 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   tr.finish(v);
 }
 
+// ----------------------------------------------------------------------------
+// LL all-reduce (IpcColl::ALLREDUCE_LL, payload <= kLLMaxBytes): one 8-byte line of the
+// payload per thread. The thread pushes its line to every peer as two 8-byte words
+// {4 data bytes, epoch} (system-scope stores into the peer's uncached LL slot, single-copy
+// atomic), then polls its own slots until every peer's two words carry this call's epoch,
+// reduces the W lines in rank order (the same bits on every rank) and writes the result.
+// No staging copy and no barrier: the slot parity alternates per call, and a rank can only
+// be at call e after receiving every peer's words of call e-1, which peers push only after
+// their call e-2 -- the last reader of this parity -- has finished.
+__device__ __forceinline__ uint64_t* ll_slot(uint32_t* sig, uint32_t parity, int src) {
+  return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(sig) + kern::kLLOffset +
+                                     ((size_t)parity * kern::kMaxRanks + (size_t)src) * kern::kLLSlotBytes);
+}
+
+__device__ __forceinline__ uint2 ll_load(const char* p, size_t off, size_t nbytes) {
+  if (off + 8 <= nbytes) return *reinterpret_cast<const uint2*>(p + off);
+  uint32_t w[2] = {0u, 0u};
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (off + k < nbytes) w[k >> 2] |= (uint32_t)(uint8_t)p[off + k] << (8 * (k & 3));
+  return make_uint2(w[0], w[1]);
+}
+
+__device__ __forceinline__ void ll_store(char* p, size_t off, size_t nbytes, uint32_t x, uint32_t y) {
+  if (off + 8 <= nbytes) {
+    *reinterpret_cast<uint2*>(p + off) = make_uint2(x, y);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (off + k < nbytes) p[off + k] = (char)(((k < 4 ? x : y) >> (8 * (k & 3))) & 0xffu);
+}
+
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ll_allreduce(IpcView v, IpcCall c) {
+  __shared__ uint32_t s_ep;
+  uint32_t* const ctl = v.counters + kern::kMaxBlocks;  // == own signal area + kLLCtlWord
+  if (threadIdx.x == 0) s_ep = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t ep = s_ep, par = ep & 1u;
+  const int me = v.rank;
+  const size_t lines = (c.bytes + 7) / 8;
+  const char* in = static_cast<const char*>(c.in[0]);
+  char* out = static_cast<char*>(c.out[0]);
+  const uint64_t tag = (uint64_t)ep << 32;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 d = ll_load(in, i * 8, c.bytes);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q == me) continue;
+      uint64_t* dst = ll_slot(v.flags[q], par, me) + 2 * i;
+      __hip_atomic_store(dst, tag | d.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(dst + 1, tag | d.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    uint4 src[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q == me) {
+        src[q] = make_uint4(d.x, d.y, 0u, 0u);
+        continue;
+      }
+      const uint64_t* p = ll_slot(v.flags[me], par, q) + 2 * i;
+      uint64_t a = 0, b = 0;
+      for (uint32_t it = 1; live; ++it) {
+        a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(a >> 32) == ep && (uint32_t)(b >> 32) == ep) break;
+        if ((it & 63u) == 0) {  // bounded spin; a host abort or another thread's timeout stops it too
+          if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+            __hip_atomic_store(v.err, 0x200u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            live = false;
+          } else if (__hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+            live = false;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      src[q] = make_uint4((uint32_t)a, (uint32_t)b, 0u, 0u);
+    }
+    const uint4 r = reduce_vec<DT, OP, W>(src, c.avg_div);
+    ll_store(out, i * 8, c.bytes, r.x, r.y);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the last block out publishes the epoch for the next LL call
+    const uint32_t done = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)
 #define PDCC_DECL_DISPATCH(DTNAME)                                                                   \
   hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,    \
@@ -472,6 +566,16 @@ hipError_t k1_by_n(const void* const* srcs, int n, void* out, size_t nbytes, int
 
 template <DType DT, RedOp OP>
 hipError_t ipc_by_w(const IpcView& v, const IpcCall& c, hipStream_t s, int grid) {
+  if (c.coll == IpcColl::ALLREDUCE_LL) {
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL((k_ll_allreduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (v.world) {
 #define PDCC_W(WW) \
   case WW: hipLaunchKernelGGL((k_ipc_reduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;

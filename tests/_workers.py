@@ -1068,3 +1068,50 @@ def split_probe(rank, size, path, device="cuda"):
     dist.all_reduce(z)
     return {"sum": x[0].item(), "want": float(sum(r + 1 for r in mine)), "bcast": y[0].item(), "root": mine[0],
             "world": z[0].item(), "grank": dist.get_rank(g), "gsize": dist.get_world_size(g)}
+
+
+def ll_probe(rank, size, device="cuda"):
+    """LL all-reduce (<= 64 KiB): every dtype/op the kernels support, odd byte counts,
+    many back-to-back calls (both slot parities, epoch rollover of the exit counter), a
+    graph-captured sequence, in-place and out-of-place -- checked against exact sums."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok = {}
+    for dt in (torch.float32, torch.bfloat16, torch.float16, torch.int32, torch.int64, torch.uint8, torch.float64):
+        for n in (1, 3, 7, 1000, 16383, (64 << 10) // torch.tensor([], dtype=dt).element_size()):
+            x = (torch.arange(n, device=d) % 5 + rank + 1).to(dt)
+            want = ((torch.arange(n, device=d) % 5) * size + size * (size + 1) // 2).to(dt)
+            dist.all_reduce(x)
+            ok[f"{dt}/{n}"] = bool(torch.equal(x, want))
+    ok["algo"] = b.last_algo() == "ipc_ll"
+    for opname in ("MAX", "MIN", "PRODUCT", "AVG"):
+        x = torch.full((777,), float(rank + 1), device=d)
+        dist.all_reduce(x, op=getattr(dist.ReduceOp, opname))
+        want = {"MAX": size, "MIN": 1, "PRODUCT": float(torch.arange(1, size + 1).prod()),
+                "AVG": (size + 1) / 2}[opname]
+        ok[opname] = bool(torch.allclose(x, torch.full_like(x, want)))
+    y = torch.zeros(4096, device=d)
+    for k in range(101):  # parities, and values that change every call
+        y.fill_(float(rank + k))
+        dist.all_reduce(y)
+        if not torch.all(y == sum(r + k for r in range(size))):
+            ok["loop"] = False
+            break
+    else:
+        ok["loop"] = True
+    from pytorch_distributed_collective_communication_amd.parallel.graphs import capture
+
+    bufs = [torch.zeros(1000 * (i + 1), device=d) for i in range(4)]
+    g = capture(lambda: [dist.all_reduce(t) for t in bufs], warmup=1)
+    for it in range(3):
+        for t in bufs:
+            t.fill_(float(rank + it))
+        g.replay()
+        torch.cuda.synchronize()
+        ok[f"graph{it}"] = all(bool(torch.all(t == sum(r + it for r in range(size)))) for t in bufs)
+    return ok

@@ -306,3 +306,19 @@ def test_split_group_on_shared_gpu(tmp_path):
     for r, got in enumerate(_gpu_launch(W.split_probe, 4, args=(str(tmp_path / "store"),))):
         assert got["sum"] == got["want"] and got["bcast"] == got["root"] and got["world"] == 4.0, got
         assert got["grank"] == r % 2 and got["gsize"] == 2, got
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ll_all_reduce_on_shared_gpu(world):
+    # small all-reduces take the LL protocol (flag-tagged pushes, no barrier): all dtypes, ops,
+    # odd sizes, 101 calls in a row, graph replay
+    for ok in _gpu_launch(W.ll_probe, world, env={"PDCC_ALGO": "ipc"}):
+        assert all(ok.values()), ok
+
+
+def test_ll_selftest_gate():
+    # a failed LL self-test leaves the 1-shot protocol in charge (and every result right)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_SELFTEST_FAIL": "1"}
+    for ok in _gpu_launch(W.ll_probe, 2, env=env):
+        assert ok.pop("algo") is False, ok
+        assert all(ok.values()), ok

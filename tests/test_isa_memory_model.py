@@ -128,3 +128,21 @@ def test_no_scratch_in_the_hot_kernels(kernels):
     for n in names:
         bad = [s for s in kernels[n] if s.startswith(("scratch_", "flat_", "s_swappc"))]  # spills, flat, calls
         assert not bad, (n, bad[:4])
+
+
+def test_ll_allreduce_words_are_single_stores_and_uncached_polls(kernels):
+    # LL (csrc/kernels/reduce_impl.h k_ll_allreduce): each {data, epoch} word must reach the
+    # peer as ONE 8-byte system-scope store (single-copy atomic: a poller never sees new
+    # data with an old epoch or the reverse), and the poll must read 8 bytes at system
+    # scope (uncached, past L2); no scratch, flat accesses or calls
+    ks = {n: b for n, b in kernels.items() if "k_ll_allreduce" in n}
+    assert len(ks) >= 7, sorted(kernels)[:20]  # one per W = 2..8 at least
+    for name, body in ks.items():
+        stores = [s for s in body if s.startswith("global_store_dwordx2") and s.endswith("sc0 sc1")]
+        polls = [s for s in body if s.startswith("global_load_dwordx2") and s.endswith("sc0 sc1")]
+        assert stores and polls, (name, [s for s in body if "sc0 sc1" in s][:8])
+        bad = [s for s in body if s.startswith(("scratch_", "flat_", "s_swappc"))]
+        assert not bad, (name, bad[:4])
+        # the data words never go out as wider stores that could tear across the epoch
+        wide = [s for s in body if s.startswith(("global_store_dwordx4", "global_store_dwordx3")) and "sc0 sc1" in s]
+        assert not wide, (name, wide[:4])

@@ -134,3 +134,9 @@ def test_split_group_distinct_gpus(tmp_path):
     for r, got in enumerate(_run(W.split_probe, 4, args=(str(tmp_path / "store"),))):
         assert got["sum"] == got["want"] and got["bcast"] == got["root"] and got["world"] == 4.0, got
         assert got["grank"] == r % 2 and got["gsize"] == 2, got
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ll_all_reduce_distinct_gpus(world):
+    for ok in _run(W.ll_probe, world, env={"PDCC_ALGO": "ipc"}):
+        assert all(ok.values()), ok

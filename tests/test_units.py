@@ -114,7 +114,8 @@ def test_rccl_env_forwarding():
 @pytest.mark.parametrize("env", [{}, {"PDCC_IPC_ZC": "0", "PDCC_IPC_ZC_MIN": "4M", "PDCC_IPC_PUSH": "0",
                                        "PDCC_IPC_ZC_CACHE": "3", "PDCC_ALGO": "ipc_push",
                                        "PDCC_RCCL_WIDE_CTAS": "56", "PDCC_RCCL_WIDE_MIN": "64M",
-                                       "PDCC_IPC_GRID": "1024", "PDCC_IPC_WIDE_GRID": "0"}])
+                                       "PDCC_IPC_GRID": "1024", "PDCC_IPC_WIDE_GRID": "0",
+                                       "PDCC_IPC_LL_MAX": "4K"}])
 def test_python_config_mirror_matches_the_backend(env):
     # the Python mirror (config.py) and the C++ Config read the same variables with the same defaults
     import re
@@ -125,7 +126,7 @@ def test_python_config_mirror_matches_the_backend(env):
     desc, py = launch(W.config_probe, 1, env=env)[0]
     cpp = dict(re.findall(r"(\w+)=(\S+)", desc))
     for key in ("ipc_1shot_max", "ipc_2shot_max", "ipc_copy_max", "ipc_max_staging", "ipc_zc", "ipc_zc_min",
-                "ipc_zc_cache", "ipc_push", "ipc_spin_ms", "ipc_grid", "ipc_wide_grid", "autotune", "autotune_sample", "algo",
+                "ipc_zc_cache", "ipc_push", "ipc_spin_ms", "ipc_grid", "ipc_wide_grid", "ipc_ll_max", "autotune", "autotune_sample", "algo",
                 "rccl_wide_ctas", "rccl_wide_min"):
         want = py[key]
         got = cpp[key].rstrip(",)")
