@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Small all-reduce latency: LL protocol vs the staged 1-shot protocol.
+
+Ranks share ONE GPU on the 1-GPU boxes (PDCC_ALGO=ipc), so this measures the
+protocols' own cost (flag round trips, staging copy, barriers), not xGMI latency.
+`--modes ll,oneshot`: ll = default (PDCC_IPC_LL_MAX=64K), oneshot = PDCC_IPC_LL_MAX=0.
+Per (mode, size): median over `--iters` of one isolated synchronous all_reduce, end to
+end (host call + kernel + the ranks' arrival skew), and the per-call time of 50
+back-to-back calls (median of 5), max over ranks. One JSON line per mode.
+
+    python scripts/ll_bench.py [--world 2] [--sizes 4,1K,16K,64K] [--iters 300]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def work(rank, size, sizes, iters):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    b = be.native_backend(None, "cuda")
+    out, ok = {}, True
+    for nbytes in sizes:
+        x = torch.full((max(1, nbytes // 4),), float(rank + 1), device=dev)
+        for _ in range(20):
+            dist.all_reduce(x)
+        x.fill_(float(rank + 1))
+        dist.all_reduce(x)
+        ok = ok and bool(torch.all(x == size * (size + 1) / 2))
+        algo = b.last_algo()
+        lat, pipe = [], []
+        for k in range(iters):  # isolated calls: launch + arrival skew + protocol
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dist.all_reduce(x)
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t0)
+        for _ in range(5):  # back-to-back calls: the protocol's per-call cost once the ranks are in step
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(50):
+                dist.all_reduce(x)
+            torch.cuda.synchronize()
+            pipe.append((time.perf_counter() - t0) / 50)
+        t = torch.tensor([statistics.median(lat), statistics.median(pipe)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[f"{nbytes}B_us"] = round(t[0].item() * 1e6, 2)
+        out[f"{nbytes}B_pipelined_us"] = round(t[1].item() * 1e6, 2)
+        out[f"{nbytes}B_algo"] = algo
+    out["correct"] = ok
+    return out
+
+
+def parse_size(s):
+    s = s.strip().upper()
+    mul = {"K": 1 << 10, "M": 1 << 20}.get(s[-1], 1)
+    return int(s[:-1] if mul > 1 else s) * mul
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--sizes", default="4,1K,16K,64K")
+    ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--modes", default="ll,oneshot")
+    a = ap.parse_args()
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+
+    sizes = [parse_size(s) for s in a.sizes.split(",")]
+    for mode in a.modes.split(","):
+        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_MAX": "64K" if mode == "ll" else "0"}
+        res = launch(work, a.world, args=(sizes, a.iters), bind_device=True, timeout_s=120, env=env,
+                     join_timeout_s=600)
+        print(json.dumps({"mode": mode, "world": a.world, **res[0]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
