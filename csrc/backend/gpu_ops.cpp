@@ -855,11 +855,30 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : (stream ? *stream : ds.stream);
   StreamSync& sy = *ds.sync;
   bool use_sig = false;
+  if (comm == cur && !cap && !stream) {
+    // a synchronous collective after async ones that may still be running on the group's
+    // comm stream: order it behind them (two collectives of one group never overlap; p2p
+    // pair streams are not waited for -- their peers may post the matching op later)
+    std::lock_guard<std::mutex> lk(sy.mu);
+    auto it = sy.comm_done.find(ds.stream.stream());
+    if (it != sy.comm_done.end() && it->second.ptr) {
+      uint64_t& seen = sy.comm_seen[cur.stream()];
+      if (seen < it->second.next) {
+        PDCC_HIP(hipStreamWaitValue64(cur.stream(), it->second.ptr, it->second.next, hipStreamWaitValueGte, ~0ull));
+        seen = it->second.next;
+      }
+    }
+  }
+  SignalWord* done_word = nullptr;
   if (comm != cur) {
     {
       std::lock_guard<std::mutex> lk(sy.mu);  // tick + enqueue under one lock: words only ever grow
-      if (sy.ok && !sy.comm_done.ptr) sy.comm_done.ptr = sy.alloc();
       if (sy.ok) {
+        done_word = &sy.comm_done[comm.stream()];  // (std::map: the reference stays valid)
+        if (!done_word->ptr) done_word->ptr = sy.alloc();
+        if (!done_word->ptr) done_word = nullptr;
+      }
+      if (sy.ok && done_word) {
         SignalWord& w = sy.user_ready[cur.stream()];
         if (!w.ptr) w.ptr = sy.alloc();
         if (w.ptr) {
@@ -900,8 +919,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   uint64_t done_tick = 0;
   if (use_sig) {
     std::lock_guard<std::mutex> lk(sy.mu);
-    done_tick = ++sy.comm_done.next;
-    PDCC_HIP(hipStreamWriteValue64(comm.stream(), sy.comm_done.ptr, done_tick, 0));
+    done_tick = ++done_word->next;
+    PDCC_HIP(hipStreamWriteValue64(comm.stream(), done_word->ptr, done_tick, 0));
   } else {
     ev = ds.events->get();
     PDCC_HIP(hipEventRecord(ev, comm.stream()));
@@ -922,7 +941,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
     }
   }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, comm,
                                            health_, cfg_.blocking_wait, timeout, std::move(ipcp), ds.events);
-  if (use_sig) w->set_signal(ds.sync, sy.comm_done.ptr, done_tick);
+  if (use_sig) w->set_signal(ds.sync, done_word->ptr, done_tick);
   if (cfg_.watchdog_ms > 0) {
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.emplace_back(w);

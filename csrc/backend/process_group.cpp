@@ -120,7 +120,7 @@ uint64_t* StreamSync::alloc() {
   return static_cast<uint64_t*>(p);
 }
 StreamSync::~StreamSync() {
-  if (comm_done.ptr) (void)hipFree(comm_done.ptr);
+  for (auto& kv : comm_done) (void)hipFree(kv.second.ptr);
   for (auto& kv : user_ready) (void)hipFree(kv.second.ptr);
 }
 

@@ -79,8 +79,13 @@ struct SignalWord {
 struct StreamSync {
   std::mutex mu;
   bool ok = true;                                // false: runtime lacks signal memory -> events
-  SignalWord comm_done;                          // written by the comm stream after each async op
+  // written by each comm / pair stream after each async op on it: one word per stream, so
+  // every word only grows (streams finish their ops in their own order)
+  std::map<hipStream_t, SignalWord> comm_done;
   std::map<hipStream_t, SignalWord> user_ready;  // written by each caller stream before an async op
+  // per caller stream: the group comm stream's tick it has already waited for (a synchronous
+  // collective on the caller's stream runs after every async collective issued before it)
+  std::map<hipStream_t, uint64_t> comm_seen;
   uint64_t* alloc();                             // nullptr when unavailable
   ~StreamSync();
 };

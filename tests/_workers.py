@@ -1115,3 +1115,26 @@ def ll_probe(rank, size, device="cuda"):
         torch.cuda.synchronize()
         ok[f"graph{it}"] = all(bool(torch.all(t == sum(r + it for r in range(size)))) for t in bufs)
     return ok
+
+
+def async_then_sync(rank, size, device="cuda", rounds=6):
+    """An async collective still running on the group's comm stream, then a synchronous
+    one on the caller's stream before wait(): the backend must order the second behind
+    the first (same-group collectives never overlap), for every engine size class."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ok = []
+    for k in range(rounds):
+        big = torch.full((4 << 20,), float(rank + k), device=d)      # 16 MiB: 2-shot / RCCL
+        mid = torch.full((1 << 20,), float(rank + 2 * k), device=d)  # 4 MiB: 2-shot
+        small = torch.full((1000,), float(rank + 3 * k), device=d)   # LL / 1-shot
+        w = dist.all_reduce(big, async_op=True)
+        dist.all_reduce(mid)
+        dist.all_reduce(small)
+        w.wait()
+        tri = size * (size - 1) / 2
+        ok.append(bool(torch.all(big == tri + size * k)) and bool(torch.all(mid == tri + 2 * size * k))
+                  and bool(torch.all(small == tri + 3 * size * k)))
+    return ok

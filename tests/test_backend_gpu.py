@@ -322,3 +322,8 @@ def test_ll_selftest_gate():
     for ok in _gpu_launch(W.ll_probe, 2, env=env):
         assert ok.pop("algo") is False, ok
         assert all(ok.values()), ok
+
+
+def test_sync_collective_after_async_is_ordered():
+    for ok in _gpu_launch(W.async_then_sync, 2, env={"PDCC_ALGO": "ipc"}):
+        assert all(ok), ok

@@ -140,3 +140,9 @@ def test_split_group_distinct_gpus(tmp_path):
 def test_ll_all_reduce_distinct_gpus(world):
     for ok in _run(W.ll_probe, world, env={"PDCC_ALGO": "ipc"}):
         assert all(ok.values()), ok
+
+
+@pytest.mark.parametrize("algo", ["rccl", "ipc", "auto"])
+def test_sync_collective_after_async_distinct_gpus(algo):
+    for ok in _run(W.async_then_sync, 2, env={"PDCC_ALGO": algo}):
+        assert all(ok), ok
