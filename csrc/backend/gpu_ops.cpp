@@ -676,6 +676,20 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
           lok = at::equal(x, base * (double)size_ + tri) && lok;
         }
       }
+      for (const int64_t m : {int64_t{3}, full}) {  // all-gather: a partial line, the maximum
+        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+        const at::Tensor in = at::full({m}, (double)rank_, opt);
+        at::Tensor out = at::full({m * size_}, -1.0, opt);
+        kern::IpcCall c{};
+        c.coll = kern::IpcColl::ALLGATHER_LL;
+        c.dtype = kern::DType::U8;
+        c.op = kern::RedOp::COPY;
+        c.bytes = in.nbytes();
+        c.in[0] = in.data_ptr();
+        for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
+        ic.launch(c, s);
+        lok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && lok;
+      }
       PDCC_HIP(hipStreamSynchronize(s));
       if (ic.error_word() != 0) {
         lok = false;
@@ -700,6 +714,10 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
   }
   ds.ipc->set_timeout_ms((uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count())));
   return true;
+}
+
+bool ProcessGroupMI355X::bytes_in_ll_range(size_t bytes) const {
+  return bytes > 0 && bytes <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes);
 }
 
 Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl_can, bool ipc_can) {
@@ -1177,8 +1195,7 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
     // small all-reduce: flag-tagged pushes, no staging copy, no barrier
-    if (!rooted && ds.ll_ok && w.nbytes() <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes))
-      c.coll = kern::IpcColl::ALLREDUCE_LL;
+    if (!rooted && ds.ll_ok && bytes_in_ll_range(w.nbytes())) c.coll = kern::IpcColl::ALLREDUCE_LL;
     c.dtype = kd;
     c.op = ko;
     c.root = root;
@@ -1250,6 +1267,11 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
     c.in[0] = wi.data_ptr();
     if (receiver)
       for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
+    if (!rooted && ds.ll_ok && bytes_in_ll_range(bytes)) {
+      c.coll = kern::IpcColl::ALLGATHER_LL;  // small: flag-tagged pushes, no staging copy, no barrier
+      ic.launch(c, s);
+      return;
+    }
     ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
@@ -1490,7 +1512,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  const bool ll = !rooted && ds.ll_ok && bytes <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes);
+  const bool ll = !rooted && ds.ll_ok && bytes_in_ll_range(bytes);
   record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
                              : one_shot                         ? "ipc_1shot"
                              : a == Algo::IPC_PUSH && !rooted ? "ipc_push"
@@ -1591,7 +1613,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     ipc(ds);
     icp = ds.ipc;
   }
-  const char* algo = a == Algo::IPC ? "ipc" : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
+  const bool ll = !rooted && ds.ll_ok && bytes_in_ll_range(wi.nbytes());
+  const char* algo = a == Algo::IPC ? (ll ? "ipc_ll" : "ipc")
+                                    : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
   auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
     enqueue_allgather(a, wi, wo, root, rooted, ds, s, to);
     if (receiver)

@@ -463,6 +463,10 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::vector<TuneRecord> autotune_table();
 
  private:
+  // payload size the LL protocol takes (PDCC_IPC_LL_MAX, at most kern::kLLMaxBytes)
+  bool bytes_in_ll_range(size_t bytes) const;
+
+ private:
   std::vector<c10::intrusive_ptr<WorkMI355X>> coalesced_cpu_;
   int (*roctx_push_)(const char*) = nullptr;
   int (*roctx_pop_)() = nullptr;

@@ -127,6 +127,7 @@ enum class IpcColl : int32_t {
   ALLREDUCE_PUSH,        // zero-copy only: push tiles to their owners' staging, owners reduce and
                          // push the result into every rank's tensor (remote writes, no remote reads)
   ALLREDUCE_LL,          // <= kLLMaxBytes: push flag-tagged words into every peer's LL slot, poll, reduce
+  ALLGATHER_LL,          // <= kLLMaxBytes per rank: the same pushes, every peer's words into its output
   kCount
 };
 

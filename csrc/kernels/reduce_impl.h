@@ -454,65 +454,106 @@ __device__ __forceinline__ void ll_store(char* p, size_t off, size_t nbytes, uin
     if (off + k < nbytes) p[off + k] = (char)(((k < 4 ? x : y) >> (8 * (k & 3))) & 0xffu);
 }
 
-template <DType DT, RedOp OP, int W>
-__global__ void __launch_bounds__(256) k_ll_allreduce(IpcView v, IpcCall c) {
+// The call's epoch (every block reads the last finished LL call's + 1) and its end (the
+// block that finishes last publishes the epoch for the next LL call on this rank).
+__device__ __forceinline__ uint32_t ll_begin(const IpcView& v) {
   __shared__ uint32_t s_ep;
+  if (threadIdx.x == 0)
+    s_ep = __hip_atomic_load(v.counters + kern::kMaxBlocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  return s_ep;
+}
+
+__device__ __forceinline__ void ll_end(const IpcView& v, uint32_t ep) {
   uint32_t* const ctl = v.counters + kern::kMaxBlocks;  // == own signal area + kLLCtlWord
-  if (threadIdx.x == 0) s_ep = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   __syncthreads();
-  const uint32_t ep = s_ep, par = ep & 1u;
-  const int me = v.rank;
-  const size_t lines = (c.bytes + 7) / 8;
-  const char* in = static_cast<const char*>(c.in[0]);
-  char* out = static_cast<char*>(c.out[0]);
-  const uint64_t tag = (uint64_t)ep << 32;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  bool live = true;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
-    const uint2 d = ll_load(in, i * 8, c.bytes);
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      if (q == me) continue;
-      uint64_t* dst = ll_slot(v.flags[q], par, me) + 2 * i;
-      __hip_atomic_store(dst, tag | d.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(dst + 1, tag | d.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    uint4 src[W];
-#pragma unroll
-    for (int q = 0; q < W; ++q) {
-      if (q == me) {
-        src[q] = make_uint4(d.x, d.y, 0u, 0u);
-        continue;
-      }
-      const uint64_t* p = ll_slot(v.flags[me], par, q) + 2 * i;
-      uint64_t a = 0, b = 0;
-      for (uint32_t it = 1; live; ++it) {
-        a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((uint32_t)(a >> 32) == ep && (uint32_t)(b >> 32) == ep) break;
-        if ((it & 63u) == 0) {  // bounded spin; a host abort or another thread's timeout stops it too
-          if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
-            __hip_atomic_store(v.err, 0x200u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            live = false;
-          } else if (__hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-            live = false;
-          }
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      src[q] = make_uint4((uint32_t)a, (uint32_t)b, 0u, 0u);
-    }
-    const uint4 r = reduce_vec<DT, OP, W>(src, c.avg_div);
-    ll_store(out, i * 8, c.bytes, r.x, r.y);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {  // the last block out publishes the epoch for the next LL call
+  if (threadIdx.x == 0) {
     const uint32_t done = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1) {
       __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// line i of this rank's payload -> slot (parity, me) of every peer, as two {data, epoch} words
+template <int W>
+__device__ __forceinline__ void ll_push(const IpcView& v, uint32_t par, uint64_t tag, size_t i, uint2 d) {
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    if (q == v.rank) continue;
+    uint64_t* dst = ll_slot(v.flags[q], par, v.rank) + 2 * i;
+    __hip_atomic_store(dst, tag | d.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, tag | d.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// wait for line i of peer q in my slot (parity, q); bounded (error word), stops on abort
+__device__ __forceinline__ uint2 ll_poll(const IpcView& v, uint32_t par, uint32_t ep, int q, size_t i, uint64_t t0,
+                                         bool& live) {
+  const uint64_t* p = ll_slot(v.flags[v.rank], par, q) + 2 * i;
+  uint64_t a = 0, b = 0;
+  for (uint32_t it = 1; live; ++it) {
+    a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((uint32_t)(a >> 32) == ep && (uint32_t)(b >> 32) == ep) break;
+    if ((it & 63u) == 0) {  // bounded spin; a host abort or another thread's timeout stops it too
+      if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+        __hip_atomic_store(v.err, 0x200u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        live = false;
+      } else if (__hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        live = false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return make_uint2((uint32_t)a, (uint32_t)b);
+}
+
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ll_allreduce(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const size_t lines = (c.bytes + 7) / 8;
+  const char* in = static_cast<const char*>(c.in[0]);
+  char* out = static_cast<char*>(c.out[0]);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 d = ll_load(in, i * 8, c.bytes);
+    ll_push<W>(v, par, tag, i, d);
+    uint4 src[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 x = q == v.rank ? d : ll_poll(v, par, ep, q, i, t0, live);
+      src[q] = make_uint4(x.x, x.y, 0u, 0u);
+    }
+    const uint4 r = reduce_vec<DT, OP, W>(src, c.avg_div);  // rank order: the same bits on every rank
+    ll_store(out, i * 8, c.bytes, r.x, r.y);
+  }
+  ll_end(v, ep);
+}
+
+// LL all-gather (IpcColl::ALLGATHER_LL, per-rank payload <= kLLMaxBytes): the same pushes,
+// every peer's lines written straight into its output (list entry or flat slice).
+template <int W>
+__global__ void __launch_bounds__(256) k_ll_allgather(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const size_t lines = (c.bytes + 7) / 8;
+  const char* in = static_cast<const char*>(c.in[0]);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 d = ll_load(in, i * 8, c.bytes);
+    ll_push<W>(v, par, tag, i, d);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 x = q == v.rank ? d : ll_poll(v, par, ep, q, i, t0, live);
+      ll_store(static_cast<char*>(c.out[q]), i * 8, c.bytes, x.x, x.y);
+    }
+  }
+  ll_end(v, ep);
 }
 
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)

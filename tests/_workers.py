@@ -1095,6 +1095,17 @@ def ll_probe(rank, size, device="cuda"):
         want = {"MAX": size, "MIN": 1, "PRODUCT": float(torch.arange(1, size + 1).prod()),
                 "AVG": (size + 1) / 2}[opname]
         ok[opname] = bool(torch.allclose(x, torch.full_like(x, want)))
+    for dt in (torch.float32, torch.bfloat16, torch.uint8, torch.int64):  # LL all-gather: list and flat outputs
+        for n in (1, 5, 999, (64 << 10) // torch.tensor([], dtype=dt).element_size()):
+            src = (torch.arange(n, device=d) % 7 + rank).to(dt)
+            outs = [torch.empty(n, dtype=dt, device=d) for _ in range(size)]
+            dist.all_gather(outs, src)
+            flat = torch.empty(n * size, dtype=dt, device=d)
+            dist.all_gather_into_tensor(flat, src)
+            want = [(torch.arange(n, device=d) % 7 + r).to(dt) for r in range(size)]
+            ok[f"ag/{dt}/{n}"] = all(bool(torch.equal(o, w)) for o, w in zip(outs, want)) and bool(
+                torch.equal(flat, torch.cat(want)))
+    ok["ag_algo"] = b.last_algo() == "ipc_ll"
     y = torch.zeros(4096, device=d)
     for k in range(101):  # parities, and values that change every call
         y.fill_(float(rank + k))

@@ -320,7 +320,7 @@ def test_ll_selftest_gate():
     # a failed LL self-test leaves the 1-shot protocol in charge (and every result right)
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_SELFTEST_FAIL": "1"}
     for ok in _gpu_launch(W.ll_probe, 2, env=env):
-        assert ok.pop("algo") is False, ok
+        assert ok.pop("algo") is False and ok.pop("ag_algo") is False, ok
         assert all(ok.values()), ok
 
 

@@ -131,12 +131,13 @@ def test_no_scratch_in_the_hot_kernels(kernels):
 
 
 def test_ll_allreduce_words_are_single_stores_and_uncached_polls(kernels):
-    # LL (csrc/kernels/reduce_impl.h k_ll_allreduce): each {data, epoch} word must reach the
+    # LL (csrc/kernels/reduce_impl.h k_ll_allreduce / k_ll_allgather): each {data, epoch} word must reach the
     # peer as ONE 8-byte system-scope store (single-copy atomic: a poller never sees new
     # data with an old epoch or the reverse), and the poll must read 8 bytes at system
     # scope (uncached, past L2); no scratch, flat accesses or calls
-    ks = {n: b for n, b in kernels.items() if "k_ll_allreduce" in n}
-    assert len(ks) >= 7, sorted(kernels)[:20]  # one per W = 2..8 at least
+    ks = {n: b for n, b in kernels.items() if "k_ll_allreduce" in n or "k_ll_allgather" in n}
+    assert sum("k_ll_allgather" in n for n in ks) == 7, sorted(ks)  # all-gather: one per W = 2..8
+    assert len(ks) >= 14, sorted(kernels)[:20]
     for name, body in ks.items():
         stores = [s for s in body if s.startswith("global_store_dwordx2") and s.endswith("sc0 sc1")]
         polls = [s for s in body if s.startswith("global_load_dwordx2") and s.endswith("sc0 sc1")]
