@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Small all-reduce latency: LL protocol vs the staged 1-shot protocol.
+"""Small all-reduce / all-gather latency: LL protocol vs the staged protocols.
 
 Ranks share ONE GPU on the 1-GPU boxes (PDCC_ALGO=ipc), so this measures the
 protocols' own cost (flag round trips, staging copy, barriers), not xGMI latency.
@@ -56,6 +56,25 @@ def work(rank, size, sizes, iters):
         out[f"{nbytes}B_us"] = round(t[0].item() * 1e6, 2)
         out[f"{nbytes}B_pipelined_us"] = round(t[1].item() * 1e6, 2)
         out[f"{nbytes}B_algo"] = algo
+        # all_gather of the same per-rank payload into a flat output
+        src = torch.full((max(1, nbytes // 4),), float(rank), device=dev)
+        flat = torch.empty(src.numel() * size, device=dev)
+        for _ in range(20):
+            dist.all_gather_into_tensor(flat, src)
+        ok = ok and bool(torch.equal(flat.view(size, -1)[:, 0].cpu(), torch.arange(size, dtype=torch.float32)))
+        ag_algo = b.last_algo()
+        pipe = []
+        for _ in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(50):
+                dist.all_gather_into_tensor(flat, src)
+            torch.cuda.synchronize()
+            pipe.append((time.perf_counter() - t0) / 50)
+        t = torch.tensor([statistics.median(pipe)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[f"ag_{nbytes}B_pipelined_us"] = round(t[0].item() * 1e6, 2)
+        out[f"ag_{nbytes}B_algo"] = ag_algo
     out["correct"] = ok
     return out
 
