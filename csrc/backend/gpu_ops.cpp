@@ -690,6 +690,49 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
         ic.launch(c, s);
         lok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && lok;
       }
+      // rooted kinds (tokens on the pairs without data), first and last rank as root, a partial line
+      for (const int root : {0, size_ - 1}) {
+        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+        const int64_t m = 1001;
+        const bool am_root = rank_ == root;
+        kern::IpcCall c{};
+        c.dtype = kern::DType::U8;
+        c.op = kern::RedOp::COPY;
+        c.root = root;
+        c.bytes = (size_t)m * 4;
+        at::Tensor b = at::full({m}, am_root ? 7.0 : -1.0, opt);  // broadcast
+        c.coll = kern::IpcColl::BROADCAST_LL;
+        c.in[0] = b.data_ptr();
+        c.out[0] = b.data_ptr();
+        ic.launch(c, s);
+        lok = at::equal(b, at::full({m}, 7.0, opt)) && lok;
+        const at::Tensor src = at::arange(size_ * m, opt).view({size_, m}).add((double)rank_);  // scatter
+        at::Tensor sc = at::full({m}, -1.0, opt);
+        c.coll = kern::IpcColl::SCATTER_LL;
+        for (int r = 0; r < size_; ++r) c.in[r] = am_root ? src[r].data_ptr() : nullptr;
+        c.out[0] = sc.data_ptr();
+        ic.launch(c, s);
+        lok = at::equal(sc, at::arange(m, opt).add((double)(rank_ * m + root))) && lok;
+        const at::Tensor gi = at::full({m}, (double)rank_, opt);  // gather
+        at::Tensor go = at::full({size_, m}, -1.0, opt);
+        c.coll = kern::IpcColl::GATHER_LL;
+        c.in[0] = gi.data_ptr();
+        for (int r = 0; r < size_; ++r) c.out[r] = am_root ? go[r].data_ptr() : nullptr;
+        ic.launch(c, s);
+        lok = (am_root ? at::equal(go, at::arange(size_, opt).view({size_, 1}).expand({size_, m}))
+                       : at::equal(go, at::full({size_, m}, -1.0, opt))) && lok;
+        const at::Tensor rb = at::arange(m, opt).remainder(5);  // reduce (non-root tensors untouched)
+        at::Tensor rx = rb + (double)(rank_ + 1);
+        c.coll = kern::IpcColl::REDUCE_LL;
+        c.dtype = kern::DType::F32;
+        c.op = kern::RedOp::SUM;
+        c.avg_div = size_;
+        c.in[0] = rx.data_ptr();
+        c.out[0] = rx.data_ptr();
+        ic.launch(c, s);
+        const double tri = size_ * (size_ + 1) / 2.0;
+        lok = at::equal(rx, am_root ? rb * (double)size_ + tri : rb + (double)(rank_ + 1)) && lok;
+      }
       PDCC_HIP(hipStreamSynchronize(s));
       if (ic.error_word() != 0) {
         lok = false;
@@ -1194,8 +1237,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
-    // small all-reduce: flag-tagged pushes, no staging copy, no barrier
-    if (!rooted && ds.ll_ok && bytes_in_ll_range(w.nbytes())) c.coll = kern::IpcColl::ALLREDUCE_LL;
+    // small (all-)reduce: flag-tagged pushes, no staging copy, no barrier
+    if (ds.ll_ok && bytes_in_ll_range(w.nbytes()))
+      c.coll = rooted ? kern::IpcColl::REDUCE_LL : kern::IpcColl::ALLREDUCE_LL;
     c.dtype = kd;
     c.op = ko;
     c.root = root;
@@ -1237,6 +1281,11 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
     c.bytes = bytes;
     c.in[0] = w.data_ptr();
     c.out[0] = w.data_ptr();
+    if (ds.ll_ok && bytes_in_ll_range(bytes)) {  // small: the root pushes flag-tagged words
+      c.coll = kern::IpcColl::BROADCAST_LL;
+      ic.launch(c, s);
+      return;
+    }
     if (c.coll == kern::IpcColl::BROADCAST_2SHOT)
       ipc_run(ds, c, w.data_ptr(), bytes, (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
     else
@@ -1267,8 +1316,8 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
     c.in[0] = wi.data_ptr();
     if (receiver)
       for (int r = 0; r < size_; ++r) c.out[r] = wo[r].data_ptr();
-    if (!rooted && ds.ll_ok && bytes_in_ll_range(bytes)) {
-      c.coll = kern::IpcColl::ALLGATHER_LL;  // small: flag-tagged pushes, no staging copy, no barrier
+    if (ds.ll_ok && bytes_in_ll_range(bytes)) {  // small: flag-tagged pushes, no staging copy, no barrier
+      c.coll = rooted ? kern::IpcColl::GATHER_LL : kern::IpcColl::ALLGATHER_LL;
       ic.launch(c, s);
       return;
     }
@@ -1330,6 +1379,11 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
     if (rank_ == root)
       for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
     c.out[0] = wo.data_ptr();
+    if (ds.ll_ok && bytes_in_ll_range(bytes)) {  // small: the root pushes chunk q to rank q
+      c.coll = kern::IpcColl::SCATTER_LL;
+      ic.launch(c, s);
+      return;
+    }
     // a flat root list (e.g. x.chunk(W)) is read in place; the other ranks share nothing
     const void* z = rank_ == root ? (is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr) : nullptr;
     ipc_run(ds, c, z, rank_ == root ? bytes * size_ : 0, kern::kTileBytes, ic.max_staging() / size_, s);
@@ -1512,7 +1566,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  const bool ll = !rooted && ds.ll_ok && bytes_in_ll_range(bytes);
+  const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
                              : one_shot                         ? "ipc_1shot"
                              : a == Algo::IPC_PUSH && !rooted ? "ipc_push"
@@ -1560,7 +1614,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     enqueue_broadcast(a, w, root, ds, s, to);
     if (!w.is_same(t) && rank_ != root) t.copy_(w);
   }, icp);
-  record(Coll::BROADCAST, a == Algo::IPC ? (one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
+  record(Coll::BROADCAST, a == Algo::IPC ? (ll ? "ipc_ll" : one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
   return work;
 }
 
@@ -1613,7 +1668,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     ipc(ds);
     icp = ds.ipc;
   }
-  const bool ll = !rooted && ds.ll_ok && bytes_in_ll_range(wi.nbytes());
+  const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
   const char* algo = a == Algo::IPC ? (ll ? "ipc_ll" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
   auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
@@ -1670,7 +1725,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
     enqueue_scatter(a, wi, wo, root, ds, s, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  record(Coll::SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
+  record(Coll::SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl", bytes, t0);
   return work;
 }
 

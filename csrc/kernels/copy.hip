@@ -321,7 +321,7 @@ size_t ipc_staging_bytes(const IpcCall& c, int world) {
     return c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH
                ? (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes : 0;
   if (c.coll == IpcColl::ALLREDUCE_PUSH) return 0;  // (zero-copy only; rejected by ipc_launch)
-  if (c.coll == IpcColl::ALLREDUCE_LL || c.coll == IpcColl::ALLGATHER_LL) return 0;  // straight into LL slots
+  if (is_ll(c.coll)) return 0;  // straight into LL slots
   const size_t cpad = (c.bytes + kTileBytes - 1) / kTileBytes * kTileBytes;
   switch (c.coll) {
     case IpcColl::SCATTER:
@@ -370,6 +370,10 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
         break;
       case IpcColl::ALLREDUCE_LL:
       case IpcColl::ALLGATHER_LL:
+      case IpcColl::REDUCE_LL:
+      case IpcColl::BROADCAST_LL:
+      case IpcColl::GATHER_LL:
+      case IpcColl::SCATTER_LL:
         g = ((c.bytes + 7) / 8 + kBlockThreads - 1) / kBlockThreads;  // one 8-byte line per thread
         break;
       default:
@@ -380,17 +384,30 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);
   if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc) return hipErrorInvalidValue;
-  if ((c.coll == IpcColl::ALLREDUCE_LL || c.coll == IpcColl::ALLGATHER_LL) &&
-      (c.zc || c.bytes == 0 || c.bytes > kLLMaxBytes))
+  if (is_ll(c.coll) && (c.zc || c.bytes == 0 || c.bytes > kLLMaxBytes))
     return hipErrorInvalidValue;
+  const bool ll_rooted = c.coll == IpcColl::REDUCE_LL || c.coll == IpcColl::BROADCAST_LL ||
+                         c.coll == IpcColl::GATHER_LL || c.coll == IpcColl::SCATTER_LL;
+  if (ll_rooted && (c.root < 0 || c.root >= v.world)) return hipErrorInvalidValue;
   const bool reducing = c.coll == IpcColl::ALLREDUCE_1SHOT || c.coll == IpcColl::ALLREDUCE_2SHOT ||
                         c.coll == IpcColl::ALLREDUCE_PUSH || c.coll == IpcColl::ALLREDUCE_LL ||
+                        c.coll == IpcColl::REDUCE_LL ||
                         c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
                         c.coll == IpcColl::REDUCE_SCATTER;
   if (c.coll == IpcColl::ALLGATHER_LL) {
     switch (v.world) {
 #define PDCC_W(WW) \
   case WW: hipLaunchKernelGGL(dev::k_ll_allgather<WW>, dim3(grid), dim3(256), 0, stream, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (c.coll == IpcColl::BROADCAST_LL || c.coll == IpcColl::GATHER_LL || c.coll == IpcColl::SCATTER_LL) {
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL(dev::k_ll_rooted<WW>, dim3(grid), dim3(256), 0, stream, v, c); break;
       PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
 #undef PDCC_W
       default: return hipErrorInvalidValue;

@@ -128,8 +128,18 @@ enum class IpcColl : int32_t {
                          // push the result into every rank's tensor (remote writes, no remote reads)
   ALLREDUCE_LL,          // <= kLLMaxBytes: push flag-tagged words into every peer's LL slot, poll, reduce
   ALLGATHER_LL,          // <= kLLMaxBytes per rank: the same pushes, every peer's words into its output
+  REDUCE_LL,             // <= kLLMaxBytes: peers push to the root only, the root reduces; tokens elsewhere
+  BROADCAST_LL,          // <= kLLMaxBytes: the root pushes to every peer; tokens elsewhere
+  GATHER_LL,             // <= kLLMaxBytes per rank: peers push to the root, the root writes out[q]
+  SCATTER_LL,            // <= kLLMaxBytes per rank: the root pushes in[q] to rank q
   kCount
 };
+
+// the flag-tagged push protocols (no staging, no barrier; payload <= kLLMaxBytes)
+inline bool is_ll(IpcColl c) {
+  return c == IpcColl::ALLREDUCE_LL || c == IpcColl::ALLGATHER_LL || c == IpcColl::REDUCE_LL ||
+         c == IpcColl::BROADCAST_LL || c == IpcColl::GATHER_LL || c == IpcColl::SCATTER_LL;
+}
 
 // Arguments of one IPC collective. `chunk_bytes` is the per-rank payload of one
 // chunk (all-gather/scatter/... operate on W chunks of that size).

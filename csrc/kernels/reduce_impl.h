@@ -556,6 +556,119 @@ __global__ void __launch_bounds__(256) k_ll_allgather(IpcView v, IpcCall c) {
   ll_end(v, ep);
 }
 
+// ----------------------------------------------------------------------------
+// Rooted LL collectives: REDUCE_LL and GATHER_LL move lines peers -> root, BROADCAST_LL and
+// SCATTER_LL root -> peers (the reference's rooted call sites, main.py:14,37,52,81, at their
+// one-element sizes). Data goes one way only, so every ordered pair of ranks that carries no
+// data exchanges a token instead: one line {0, epoch} in the same slot. Each rank then still
+// hears from every peer in every LL call, which keeps the parity argument above valid for any
+// sequence of LL kinds. Block 0's thread 0 pushes the tokens at entry and polls the expected
+// ones before it exits, so the call ends only once every peer has entered it.
+__device__ __forceinline__ void ll_push_one(const IpcView& v, int q, uint32_t par, uint64_t tag, size_t i, uint2 d) {
+  uint64_t* dst = ll_slot(v.flags[q], par, v.rank) + 2 * i;
+  __hip_atomic_store(dst, tag | d.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(dst + 1, tag | d.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// up: data flows peers -> root (reduce, gather); otherwise root -> peers (broadcast, scatter)
+__device__ __forceinline__ bool ll_sends_data(int me, int q, int root, bool up) { return up ? q == root : me == root; }
+
+template <int W>
+__device__ __forceinline__ void ll_tokens_push(const IpcView& v, uint32_t par, uint64_t tag, int root, bool up) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+#pragma unroll
+  for (int q = 0; q < W; ++q)
+    if (q != v.rank && !ll_sends_data(v.rank, q, root, up)) ll_push_one(v, q, par, tag, 0, make_uint2(0u, 0u));
+}
+
+template <int W>
+__device__ __forceinline__ void ll_tokens_poll(const IpcView& v, uint32_t par, uint32_t ep, int root, bool up,
+                                               uint64_t t0, bool& live) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+#pragma unroll
+  for (int q = 0; q < W; ++q)
+    if (q != v.rank && !ll_sends_data(q, v.rank, root, up)) (void)ll_poll(v, par, ep, q, 0, t0, live);
+}
+
+// REDUCE_LL: peers push their lines to the root only; the root reduces in rank order into
+// out[0]. Non-root tensors are left untouched.
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ll_reduce(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const bool am_root = v.rank == c.root;
+  ll_tokens_push<W>(v, par, tag, c.root, true);
+  const size_t lines = (c.bytes + 7) / 8;
+  const char* in = static_cast<const char*>(c.in[0]);
+  char* out = static_cast<char*>(c.out[0]);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    const uint2 d = ll_load(in, i * 8, c.bytes);
+    if (!am_root) {
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        if (q == c.root) ll_push_one(v, q, par, tag, i, d);
+      continue;
+    }
+    uint4 src[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 x = q == v.rank ? d : ll_poll(v, par, ep, q, i, t0, live);
+      src[q] = make_uint4(x.x, x.y, 0u, 0u);
+    }
+    const uint4 r = reduce_vec<DT, OP, W>(src, c.avg_div);
+    ll_store(out, i * 8, c.bytes, r.x, r.y);
+  }
+  ll_tokens_poll<W>(v, par, ep, c.root, true, t0, live);
+  ll_end(v, ep);
+}
+
+// BROADCAST_LL (root: in[0] = out[0] = the tensor), SCATTER_LL (root: in[q] = chunk for rank q),
+// GATHER_LL (root: out[q] = slot for rank q's input); c.bytes = per-rank payload.
+template <int W>
+__global__ void __launch_bounds__(256) k_ll_rooted(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const int root = c.root;
+  const bool am_root = v.rank == root, up = c.coll == IpcColl::GATHER_LL;
+  ll_tokens_push<W>(v, par, tag, root, up);
+  const size_t lines = (c.bytes + 7) / 8;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    if (up) {  // gather
+      const uint2 d = ll_load(static_cast<const char*>(c.in[0]), i * 8, c.bytes);
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        if (!am_root) {
+          if (q == root) ll_push_one(v, q, par, tag, i, d);
+        } else {
+          const uint2 x = q == v.rank ? d : ll_poll(v, par, ep, q, i, t0, live);
+          ll_store(static_cast<char*>(c.out[q]), i * 8, c.bytes, x.x, x.y);
+        }
+      }
+    } else if (am_root) {  // broadcast / scatter, root side
+      const bool scatter = c.coll == IpcColl::SCATTER_LL;
+      const uint2 d0 = ll_load(static_cast<const char*>(c.in[0]), i * 8, c.bytes);
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const uint2 d = scatter && q > 0 ? ll_load(static_cast<const char*>(c.in[q]), i * 8, c.bytes) : d0;
+        if (q != v.rank) ll_push_one(v, q, par, tag, i, d);
+        else if (scatter) ll_store(static_cast<char*>(c.out[0]), i * 8, c.bytes, d.x, d.y);
+      }
+    } else {  // broadcast / scatter, receiving side: only the root's slot carries data
+      uint2 x = make_uint2(0u, 0u);
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        if (q == root) x = ll_poll(v, par, ep, q, i, t0, live);
+      ll_store(static_cast<char*>(c.out[0]), i * 8, c.bytes, x.x, x.y);
+    }
+  }
+  ll_tokens_poll<W>(v, par, ep, root, up, t0, live);
+  ll_end(v, ep);
+}
+
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)
 #define PDCC_DECL_DISPATCH(DTNAME)                                                                   \
   hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,    \
@@ -611,6 +724,16 @@ hipError_t ipc_by_w(const IpcView& v, const IpcCall& c, hipStream_t s, int grid)
     switch (v.world) {
 #define PDCC_W(WW) \
   case WW: hipLaunchKernelGGL((k_ll_allreduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (c.coll == IpcColl::REDUCE_LL) {
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL((k_ll_reduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
       PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
 #undef PDCC_W
       default: return hipErrorInvalidValue;

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Small all-reduce / all-gather latency: LL protocol vs the staged protocols.
+"""Small-message latency of all six collectives: LL protocol vs the staged protocols.
 
 Ranks share ONE GPU on the 1-GPU boxes (PDCC_ALGO=ipc), so this measures the
 protocols' own cost (flag round trips, staging copy, barriers), not xGMI latency.
@@ -75,6 +75,37 @@ def work(rank, size, sizes, iters):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         out[f"ag_{nbytes}B_pipelined_us"] = round(t[0].item() * 1e6, 2)
         out[f"ag_{nbytes}B_algo"] = ag_algo
+        # the rooted collectives of the reference (main.py:14,37,52,81), root 0, same per-rank payload
+        n = max(1, nbytes // 4)
+        y = torch.full((n,), float(rank + 1), device=dev)
+        glist = [torch.empty(n, device=dev) for _ in range(size)] if rank == 0 else None
+        slist = [torch.full((n,), float(r), device=dev) for r in range(size)] if rank == 0 else None
+        s_out = torch.empty(n, device=dev)
+        rooted = {
+            "reduce": lambda: dist.reduce(y, dst=0),
+            "broadcast": lambda: dist.broadcast(y, src=0),
+            "gather": lambda: dist.gather(src, gather_list=glist, dst=0),
+            "scatter": lambda: dist.scatter(s_out, scatter_list=slist, src=0),
+        }
+        for name, fn in rooted.items():
+            for _ in range(20):
+                fn()
+            r_algo = b.last_algo()
+            pipe = []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(50):
+                    fn()
+                torch.cuda.synchronize()
+                pipe.append((time.perf_counter() - t0) / 50)
+            t = torch.tensor([statistics.median(pipe)], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            out[f"{name}_{nbytes}B_pipelined_us"] = round(t[0].item() * 1e6, 2)
+            out[f"{name}_{nbytes}B_algo"] = r_algo
+        ok = ok and bool(torch.all(s_out == rank))
+        if rank == 0:
+            ok = ok and all(bool(torch.all(g == r)) for r, g in enumerate(glist))
     out["correct"] = ok
     return out
 

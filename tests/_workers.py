@@ -1128,6 +1128,85 @@ def ll_probe(rank, size, device="cuda"):
     return ok
 
 
+def ll_rooted_probe(rank, size, device="cuda", iters=61):
+    """Rooted LL collectives (reduce / broadcast / gather / scatter <= 64 KiB per rank): the
+    reference's one-element demos, odd byte counts, every root, and a long interleaved run of
+    all six kinds with the root moving every call (the token lines must keep every slot
+    parity safe whatever the sequence), plus a graph-captured rooted sequence."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok, algos = {}, {}
+    tri = size * (size + 1) / 2
+
+    def run_all(n, root, k, dt=torch.float32):
+        res = {}
+        x = torch.full((n,), float(rank + 1 + k), device=d).to(dt)
+        keep = x.clone()
+        dist.reduce(x, dst=root)
+        res["reduce"] = bool(torch.equal(x, torch.full_like(x, tri + size * k))) if rank == root else bool(
+            torch.equal(x, keep))
+        algos["reduce"] = b.last_algo()
+        y = (torch.arange(n, device=d) % 9 + k).to(dt) if rank == root else torch.full((n,), -1.0, device=d).to(dt)
+        dist.broadcast(y, src=root)
+        res["broadcast"] = bool(torch.equal(y, (torch.arange(n, device=d) % 9 + k).to(dt)))
+        algos["broadcast"] = b.last_algo()
+        g_in = torch.full((n,), float(rank + k), device=d).to(dt)
+        g_out = [torch.full((n,), -1.0, device=d).to(dt) for _ in range(size)] if rank == root else None
+        dist.gather(g_in, gather_list=g_out, dst=root)
+        if rank == root:
+            res["gather"] = all(bool(torch.all(t == r + k)) for r, t in enumerate(g_out))
+        algos["gather"] = b.last_algo()
+        s_out = torch.full((n,), -1.0, device=d).to(dt)
+        s_in = [torch.full((n,), float(10 * r + k), device=d).to(dt) for r in range(size)] if rank == root else None
+        dist.scatter(s_out, scatter_list=s_in, src=root)
+        res["scatter"] = bool(torch.all(s_out == 10 * rank + k))
+        algos["scatter"] = b.last_algo()
+        return res
+
+    # the reference's demo sizes (main.py: one element) with every root, then odd and maximal sizes
+    for root in range(size):
+        for key, v in run_all(1, root, 0).items():
+            ok[f"one/{root}/{key}"] = v
+    for dt in (torch.float32, torch.bfloat16, torch.uint8):
+        es = torch.tensor([], dtype=dt).element_size()
+        for n in (3, 1001, (64 << 10) // es):
+            for key, v in run_all(n, size - 1, 1, dt).items():
+                ok[f"{dt}/{n}/{key}"] = v
+    ok["algos"] = all(a == "ipc_ll" for a in algos.values()) or algos
+    # interleaved: the root and the kind change every call, all-reduce / all-gather in between
+    good = True
+    for k in range(iters):
+        root = (k * 7 + 3) % size
+        good = all(run_all(1 + (k * 37) % 2000, root, k).values()) and good
+        z = torch.full((513,), float(rank + k), device=d)
+        dist.all_reduce(z)
+        good = good and bool(torch.all(z == size * (size - 1) / 2 + size * k))
+    ok["interleaved"] = good
+    from pytorch_distributed_collective_communication_amd.parallel.graphs import capture
+
+    bx = torch.zeros(700, device=d)
+    rx = torch.zeros(300, device=d)
+
+    def step():
+        dist.broadcast(bx, src=size - 1)
+        dist.reduce(rx, dst=0)
+
+    g = capture(step, warmup=1)
+    for it in range(3):
+        bx.fill_(float(100 + it) if rank == size - 1 else -1.0)
+        rx.fill_(float(rank + it))
+        g.replay()
+        torch.cuda.synchronize()
+        ok[f"graph{it}"] = bool(torch.all(bx == 100 + it)) and (
+            bool(torch.all(rx == size * (size - 1) / 2 + size * it)) if rank == 0 else bool(torch.all(rx == rank + it)))
+    return ok
+
+
 def async_then_sync(rank, size, device="cuda", rounds=6):
     """An async collective still running on the group's comm stream, then a synchronous
     one on the caller's stream before wait(): the backend must order the second behind

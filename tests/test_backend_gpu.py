@@ -324,6 +324,24 @@ def test_ll_selftest_gate():
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_ll_rooted_collectives_on_shared_gpu(world):
+    # small reduce / broadcast / gather / scatter take the rooted LL kernels (data one way,
+    # token lines on the other pairs): every root, odd sizes, a long interleaved run, graph replay
+    for ok in _gpu_launch(W.ll_rooted_probe, world, env={"PDCC_ALGO": "ipc"}):
+        assert ok.pop("algos") is True, ok
+        assert all(ok.values()), ok
+
+
+def test_ll_rooted_selftest_gate():
+    # with the LL self-test failed the rooted collectives take the staged 1-shot protocols
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_SELFTEST_FAIL": "0"}
+    for ok in _gpu_launch(W.ll_rooted_probe, 2, args=("cuda", 8), env=env):
+        algos = ok.pop("algos")
+        assert isinstance(algos, dict) and "ipc_ll" not in algos.values(), algos
+        assert all(ok.values()), ok
+
+
 def test_sync_collective_after_async_is_ordered():
     for ok in _gpu_launch(W.async_then_sync, 2, env={"PDCC_ALGO": "ipc"}):
         assert all(ok), ok

@@ -135,9 +135,13 @@ def test_ll_allreduce_words_are_single_stores_and_uncached_polls(kernels):
     # peer as ONE 8-byte system-scope store (single-copy atomic: a poller never sees new
     # data with an old epoch or the reverse), and the poll must read 8 bytes at system
     # scope (uncached, past L2); no scratch, flat accesses or calls
-    ks = {n: b for n, b in kernels.items() if "k_ll_allreduce" in n or "k_ll_allgather" in n}
+    # (and the rooted k_ll_reduce / k_ll_rooted: data one way, token lines on the other pairs)
+    ks = {n: b for n, b in kernels.items() if any(k in n for k in ("k_ll_allreduce", "k_ll_allgather", "k_ll_reduce",
+                                                                 "k_ll_rooted"))}
     assert sum("k_ll_allgather" in n for n in ks) == 7, sorted(ks)  # all-gather: one per W = 2..8
-    assert len(ks) >= 14, sorted(kernels)[:20]
+    assert sum("k_ll_rooted" in n for n in ks) == 7, sorted(ks)  # broadcast / gather / scatter: one per W
+    assert sum("k_ll_reduce" in n for n in ks) >= 7, sorted(ks)
+    assert len(ks) >= 28, sorted(kernels)[:20]
     for name, body in ks.items():
         stores = [s for s in body if s.startswith("global_store_dwordx2") and s.endswith("sc0 sc1")]
         polls = [s for s in body if s.startswith("global_load_dwordx2") and s.endswith("sc0 sc1")]
