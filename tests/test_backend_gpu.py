@@ -333,6 +333,22 @@ def test_ll_rooted_collectives_on_shared_gpu(world):
         assert all(ok.values()), ok
 
 
+def test_shared_gpu_world8():
+    # W = 8, the rank count of a full MI355X node, on one GPU: the W = 8 instantiations of the IPC
+    # kernels the 8-GPU bench runs (golden outputs, bulk 1-/2-shot with chunking, all six LL kinds)
+    env = {"PDCC_ALGO": "ipc"}
+    res = _gpu_launch(W.golden, 8, env=env)
+    for r, got in enumerate(res):
+        assert got == W.expected_golden(r, 8), (r, got)
+    for ok in _gpu_launch(W.large, 8, args=("cuda", 300_007), env={**env, "PDCC_IPC_MAX_STAGING": "2M"}):
+        assert all(ok.values()), ok
+    for ok in _gpu_launch(W.zero_copy, 8, env={**env, "PDCC_IPC_1SHOT_MAX": "256K"}):
+        assert all(ok.values()), ok
+    for ok in _gpu_launch(W.ll_rooted_probe, 8, args=("cuda", 12), env=env):
+        assert ok.pop("algos") is True, ok
+        assert all(ok.values()), ok
+
+
 def test_ll_rooted_selftest_gate():
     # with the LL self-test failed the rooted collectives take the staged 1-shot protocols
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_SELFTEST_FAIL": "0"}
