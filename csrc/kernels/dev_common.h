@@ -233,6 +233,12 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
       } else if (lane_off < lim) {
         store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
       }
+      // The counted waits assume one store per consume. A wave with nothing to store
+      // here (its 1 KiB lies past `lim`: a padding tile of a partial last 2-shot row,
+      // the tail of a ragged tile) issues none, which would leave every later wait one
+      // op too loose -- a younger tile's LDS slot could be read while its DMA is still
+      // in flight. Drain instead: the later waits are then exact or stricter.
+      if ((size_t)wave * kWaveBytes >= lim) drain_vm();
     } else {
 #pragma unroll
       for (int j = 0; j < NDST; ++j) *reinterpret_cast<uint4*>(m.dst(j, i) + lane_off) = r;

@@ -1207,6 +1207,32 @@ def ll_rooted_probe(rank, size, device="cuda", iters=61):
     return ok
 
 
+def partial_rows(rank, size, device="cuda", reps=6):
+    """2-shot all-reduces whose last row of W tiles is partial (the padding tiles of that row
+    are skipped by the pull pipeline), mixed with other sizes so every block's LDS ring holds
+    stale tiles from earlier rows: every result must be exact, on the IPC 2-shot engine."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok, algos = {}, set()
+    tri = size * (size + 1) / 2
+    sizes = (1 << 20, 3 * size * 1024 + 257, (5 * size + size - 1) * 1024 + 100, (1 << 20) + 3 * 1024)
+    for k in range(reps):
+        for n in sizes:
+            base = torch.arange(n, device=d).remainder(7).float()
+            x = base + (rank + 1 + k)
+            dist.all_reduce(x)
+            algos.add(b.last_algo())
+            key = f"{n}"
+            ok[key] = ok.get(key, True) and bool(torch.equal(x, base * size + tri + size * k))
+    ok["algos"] = all(a.startswith("ipc_2shot") for a in algos) or sorted(algos)
+    return ok
+
+
 def async_then_sync(rank, size, device="cuda", rounds=6):
     """An async collective still running on the group's comm stream, then a synchronous
     one on the caller's stream before wait(): the backend must order the second behind

@@ -333,6 +333,16 @@ def test_ll_rooted_collectives_on_shared_gpu(world):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world,zc", [(5, "0"), (7, "0"), (7, "1"), (8, "0")])
+def test_two_shot_partial_last_row(world, zc):
+    # regression: a padding tile of a partial last 2-shot row stores nothing, and the LDS-DMA
+    # pipeline's counted waits must not go one op loose after it (stale tiles from earlier rows)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC": zc, "PDCC_IPC_LL_MAX": "0", "PDCC_IPC_1SHOT_MAX": "0"}
+    for ok in _gpu_launch(W.partial_rows, world, env=env):
+        assert ok.pop("algos") is True, ok
+        assert all(ok.values()), ok
+
+
 def test_shared_gpu_world8():
     # W = 8, the rank count of a full MI355X node, on one GPU: the W = 8 instantiations of the IPC
     # kernels the 8-GPU bench runs (golden outputs, bulk 1-/2-shot with chunking, all six LL kinds)

@@ -142,6 +142,14 @@ def test_ll_all_reduce_distinct_gpus(world):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ll_rooted_distinct_gpus(world):
+    # reduce / broadcast / gather / scatter LL kernels over xGMI: data one way, tokens on the other pairs
+    for ok in _run(W.ll_rooted_probe, world, env={"PDCC_ALGO": "ipc"}):
+        assert ok.pop("algos") is True, ok
+        assert all(ok.values()), ok
+
+
 @pytest.mark.parametrize("algo", ["rccl", "ipc", "auto"])
 def test_sync_collective_after_async_distinct_gpus(algo):
     for ok in _run(W.async_then_sync, 2, env={"PDCC_ALGO": algo}):
