@@ -44,6 +44,33 @@ def work(rank, size, reps):
         y = torch.full((5000,), float(rank + k), device=d) if rank == 0 else torch.zeros(5000, device=d)
         dist.broadcast(y, src=0)
         note("broadcast_5000", y, torch.full((5000,), float(k), device=d))
+        # ragged bulk sizes (partial rows / tiles) through the rooted and chunked collectives
+        nb = (1 << 20) + 3 * 1024 + 5
+        root = (k * 3 + 1) % size
+        base = torch.arange(nb, device=d).remainder(7).float()
+        z = base + (rank + 1 + k)
+        dist.reduce(z, dst=root)
+        note("reduce_big", z, base * size + tri + size * k if rank == root else base + (rank + 1 + k))
+        z = base + k if rank == root else torch.zeros(nb, device=d)
+        dist.broadcast(z, src=root)
+        note("broadcast_big", z, base + k)
+        mb = (1 << 18) + 1031
+        ins = [torch.full((mb,), float(100 * rank + q + k), device=d) for q in range(size)]
+        o = torch.empty(mb, device=d)
+        dist.reduce_scatter(o, ins)
+        note("reduce_scatter_big", o, torch.full((mb,), float(100 * tri - 100 * size + size * (rank + k)), device=d))
+        outs = [torch.empty(mb, device=d) for _ in range(size)]
+        dist.all_to_all(outs, ins)
+        note("all_to_all_big", torch.stack(outs),
+             torch.stack([torch.full((mb,), float(100 * q + rank + k), device=d) for q in range(size)]))
+        g = [torch.empty(mb, device=d) for _ in range(size)] if rank == root else None
+        dist.gather(ins[0], gather_list=g, dst=root)
+        if rank == root:
+            note("gather_big", torch.stack(g), torch.stack([torch.full((mb,), float(100 * q + k), device=d)
+                                                            for q in range(size)]))
+        s_in = [torch.full((mb,), float(10 * q + k), device=d) for q in range(size)] if rank == root else None
+        dist.scatter(o, scatter_list=s_in, src=root)
+        note("scatter_big", o, torch.full((mb,), float(10 * rank + k), device=d))
     torch.cuda.synchronize()
     return res
 
