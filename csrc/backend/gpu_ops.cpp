@@ -733,6 +733,31 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
         const double tri = size_ * (size_ + 1) / 2.0;
         lok = at::equal(rx, am_root ? rb * (double)size_ + tri : rb + (double)(rank_ + 1)) && lok;
       }
+      {  // reduce-scatter and all-to-all: chunk q to rank q (a partial line per chunk)
+        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+        const int64_t m = 333;
+        const at::Tensor src = at::arange(size_, opt).view({size_, 1}).add((double)(100 * rank_)).expand({size_, m})
+                                   .contiguous();  // chunk q = 100 * rank + q
+        at::Tensor rs = at::full({m}, -1.0, opt);
+        at::Tensor a2a = at::full({size_, m}, -1.0, opt);
+        kern::IpcCall c{};
+        c.coll = kern::IpcColl::REDUCE_SCATTER_LL;
+        c.dtype = kern::DType::F32;
+        c.op = kern::RedOp::SUM;
+        c.avg_div = size_;
+        c.bytes = (size_t)m * 4;
+        for (int r = 0; r < size_; ++r) c.in[r] = src[r].data_ptr();
+        c.out[0] = rs.data_ptr();
+        ic.launch(c, s);
+        lok = at::equal(rs, at::full({m}, 100.0 * (tri - size_) + (double)(size_ * rank_), opt)) && lok;
+        c.coll = kern::IpcColl::ALLTOALL_LL;
+        c.dtype = kern::DType::U8;
+        c.op = kern::RedOp::COPY;
+        for (int r = 0; r < size_; ++r) c.out[r] = a2a[r].data_ptr();
+        ic.launch(c, s);
+        lok = at::equal(a2a, at::arange(size_, opt).mul(100.0).add((double)rank_).view({size_, 1}).expand({size_, m}))
+              && lok;
+      }
       PDCC_HIP(hipStreamSynchronize(s));
       if (ic.error_word() != 0) {
         lok = false;
@@ -1430,6 +1455,11 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
     c.zstride = bytes;
     for (int r = 0; r < size_; ++r) c.in[r] = wi[r].data_ptr();
     c.out[0] = wo.data_ptr();
+    if (ds.ll_ok && bytes_in_ll_range(bytes)) {  // small: chunk q pushed to rank q, reduced there
+      c.coll = kern::IpcColl::REDUCE_SCATTER_LL;
+      ic.launch(c, s);
+      return;
+    }
     // a flat input (reduce_scatter_tensor) is read in place by every peer
     ipc_run(ds, c, is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr, bytes * size_, kern::kTileBytes,
             ic.max_staging() / size_, s);
@@ -1477,6 +1507,11 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
     for (int r = 0; r < size_; ++r) {
       c.in[r] = wi[r].data_ptr();
       c.out[r] = wo[r].data_ptr();
+    }
+    if (ds.ll_ok && bytes_in_ll_range(c.bytes)) {  // small: chunk q pushed straight to rank q
+      c.coll = kern::IpcColl::ALLTOALL_LL;
+      ic.launch(c, s);
+      return;
     }
     ipc_run(ds, c, is_flat(wi, c.bytes) ? wi[0].data_ptr() : nullptr, c.bytes * size_, kern::kTileBytes,
             ic.max_staging() / size_, s);
@@ -1781,7 +1816,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, ds, s, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  record(Coll::REDUCE_SCATTER, a == Algo::IPC ? "ipc" : "rccl", bytes, t0);
+  record(Coll::REDUCE_SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
+         bytes, t0);
   return work;
 }
 
@@ -1836,7 +1872,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     for (size_t i = 0; i < outs.size(); ++i)
       if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
   }, icp);
-  record(Coll::ALLTOALL, a == Algo::IPC ? "ipc" : "rccl", total, t0);
+  record(Coll::ALLTOALL, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(chunk) ? "ipc_ll" : "ipc") : "rccl", total,
+         t0);
   return work;
 }
 

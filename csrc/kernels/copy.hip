@@ -374,6 +374,8 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
       case IpcColl::BROADCAST_LL:
       case IpcColl::GATHER_LL:
       case IpcColl::SCATTER_LL:
+      case IpcColl::REDUCE_SCATTER_LL:
+      case IpcColl::ALLTOALL_LL:
         g = ((c.bytes + 7) / 8 + kBlockThreads - 1) / kBlockThreads;  // one 8-byte line per thread
         break;
       default:
@@ -391,13 +393,23 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   if (ll_rooted && (c.root < 0 || c.root >= v.world)) return hipErrorInvalidValue;
   const bool reducing = c.coll == IpcColl::ALLREDUCE_1SHOT || c.coll == IpcColl::ALLREDUCE_2SHOT ||
                         c.coll == IpcColl::ALLREDUCE_PUSH || c.coll == IpcColl::ALLREDUCE_LL ||
-                        c.coll == IpcColl::REDUCE_LL ||
+                        c.coll == IpcColl::REDUCE_LL || c.coll == IpcColl::REDUCE_SCATTER_LL ||
                         c.coll == IpcColl::REDUCE_1SHOT || c.coll == IpcColl::REDUCE_2SHOT ||
                         c.coll == IpcColl::REDUCE_SCATTER;
   if (c.coll == IpcColl::ALLGATHER_LL) {
     switch (v.world) {
 #define PDCC_W(WW) \
   case WW: hipLaunchKernelGGL(dev::k_ll_allgather<WW>, dim3(grid), dim3(256), 0, stream, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (c.coll == IpcColl::ALLTOALL_LL) {
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL(dev::k_ll_alltoall<WW>, dim3(grid), dim3(256), 0, stream, v, c); break;
       PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
 #undef PDCC_W
       default: return hipErrorInvalidValue;

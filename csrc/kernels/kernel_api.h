@@ -132,13 +132,16 @@ enum class IpcColl : int32_t {
   BROADCAST_LL,          // <= kLLMaxBytes: the root pushes to every peer; tokens elsewhere
   GATHER_LL,             // <= kLLMaxBytes per rank: peers push to the root, the root writes out[q]
   SCATTER_LL,            // <= kLLMaxBytes per rank: the root pushes in[q] to rank q
+  REDUCE_SCATTER_LL,     // <= kLLMaxBytes per chunk: in[q] pushed to rank q, reduced there
+  ALLTOALL_LL,           // <= kLLMaxBytes per chunk: in[q] pushed to rank q, written to its out[src]
   kCount
 };
 
 // the flag-tagged push protocols (no staging, no barrier; payload <= kLLMaxBytes)
 inline bool is_ll(IpcColl c) {
   return c == IpcColl::ALLREDUCE_LL || c == IpcColl::ALLGATHER_LL || c == IpcColl::REDUCE_LL ||
-         c == IpcColl::BROADCAST_LL || c == IpcColl::GATHER_LL || c == IpcColl::SCATTER_LL;
+         c == IpcColl::BROADCAST_LL || c == IpcColl::GATHER_LL || c == IpcColl::SCATTER_LL ||
+         c == IpcColl::REDUCE_SCATTER_LL || c == IpcColl::ALLTOALL_LL;
 }
 
 // Arguments of one IPC collective. `chunk_bytes` is the per-rank payload of one

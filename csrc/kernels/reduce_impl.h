@@ -669,6 +669,61 @@ __global__ void __launch_bounds__(256) k_ll_rooted(IpcView v, IpcCall c) {
   ll_end(v, ep);
 }
 
+// REDUCE_SCATTER_LL / ALLTOALL_LL (per-chunk payload <= kLLMaxBytes): chunk q of every rank
+// (c.in[q]) is pushed to rank q only. Every ordered pair of ranks carries data, so the reuse
+// argument of the all-reduce holds without tokens. Reduce-scatter reduces the W chunks
+// addressed to this rank in rank order into out[0]; all-to-all writes chunk-from-q to out[q].
+template <DType DT, RedOp OP, int W>
+__global__ void __launch_bounds__(256) k_ll_reduce_scatter(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const size_t lines = (c.bytes + 7) / 8;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+    uint2 own = make_uint2(0u, 0u);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 d = ll_load(static_cast<const char*>(c.in[q]), i * 8, c.bytes);
+      if (q == v.rank) own = d;
+      else ll_push_one(v, q, par, tag, i, d);
+    }
+    uint4 src[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 x = q == v.rank ? own : ll_poll(v, par, ep, q, i, t0, live);
+      src[q] = make_uint4(x.x, x.y, 0u, 0u);
+    }
+    const uint4 r = reduce_vec<DT, OP, W>(src, c.avg_div);
+    ll_store(static_cast<char*>(c.out[0]), i * 8, c.bytes, r.x, r.y);
+  }
+  ll_end(v, ep);
+}
+
+template <int W>
+__global__ void __launch_bounds__(256) k_ll_alltoall(IpcView v, IpcCall c) {
+  const uint32_t ep = ll_begin(v), par = ep & 1u;
+  const uint64_t tag = (uint64_t)ep << 32;
+  const size_t lines = (c.bytes + 7) / 8;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool live = true;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < lines; i += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const uint2 d = ll_load(static_cast<const char*>(c.in[q]), i * 8, c.bytes);
+      if (q == v.rank) ll_store(static_cast<char*>(c.out[q]), i * 8, c.bytes, d.x, d.y);
+      else ll_push_one(v, q, par, tag, i, d);
+    }
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q == v.rank) continue;
+      const uint2 x = ll_poll(v, par, ep, q, i, t0, live);
+      ll_store(static_cast<char*>(c.out[q]), i * 8, c.bytes, x.x, x.y);
+    }
+  }
+  ll_end(v, ep);
+}
+
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)
 #define PDCC_DECL_DISPATCH(DTNAME)                                                                   \
   hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,    \
@@ -734,6 +789,16 @@ hipError_t ipc_by_w(const IpcView& v, const IpcCall& c, hipStream_t s, int grid)
     switch (v.world) {
 #define PDCC_W(WW) \
   case WW: hipLaunchKernelGGL((k_ll_reduce<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
+      PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
+#undef PDCC_W
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  if (c.coll == IpcColl::REDUCE_SCATTER_LL) {
+    switch (v.world) {
+#define PDCC_W(WW) \
+  case WW: hipLaunchKernelGGL((k_ll_reduce_scatter<DT, OP, WW>), dim3(grid), dim3(256), 0, s, v, c); break;
       PDCC_W(2) PDCC_W(3) PDCC_W(4) PDCC_W(5) PDCC_W(6) PDCC_W(7) PDCC_W(8)
 #undef PDCC_W
       default: return hipErrorInvalidValue;

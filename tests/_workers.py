@@ -1207,6 +1207,60 @@ def ll_rooted_probe(rank, size, device="cuda", iters=61):
     return ok
 
 
+def ll_exchange_probe(rank, size, device="cuda", iters=41):
+    """LL reduce_scatter / all_to_all (<= 64 KiB per chunk): list and flat forms, dtypes, odd
+    sizes, ops, and a long run interleaved with the other LL kinds."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok, algos = {}, {}
+    tri0 = size * (size - 1) / 2  # sum of ranks
+
+    def rs_a2a(n, k, dt=torch.float32, op="SUM"):
+        res = {}
+        ins = [torch.full((n,), float(10 * rank + q + k), device=d).to(dt) for q in range(size)]
+        o = torch.full((n,), -1.0, device=d).to(dt)
+        dist.reduce_scatter(o, ins, op=getattr(dist.ReduceOp, op))
+        vals = [10 * s + rank + k for s in range(size)]
+        want = {"SUM": sum(vals), "MAX": max(vals), "MIN": min(vals)}[op]
+        res["rs"] = bool(torch.all(o == want))
+        algos["rs"] = b.last_algo()
+        flat_out = torch.empty(n, device=d).to(dt)
+        dist.reduce_scatter_tensor(flat_out, torch.cat(ins))
+        res["rs_flat"] = bool(torch.all(flat_out == sum(vals)))
+        outs = [torch.full((n,), -1.0, device=d).to(dt) for _ in range(size)]
+        dist.all_to_all(outs, ins)
+        res["a2a"] = all(bool(torch.all(t == 10 * q + rank + k)) for q, t in enumerate(outs))
+        algos["a2a"] = b.last_algo()
+        fo = torch.empty(n * size, device=d).to(dt)
+        dist.all_to_all_single(fo, torch.cat(ins))
+        res["a2a_flat"] = all(bool(torch.all(t == 10 * q + rank + k)) for q, t in enumerate(fo.view(size, n)))
+        return res
+
+    for dt in (torch.float32, torch.bfloat16, torch.int32):
+        es = torch.tensor([], dtype=dt).element_size()
+        for n in (1, 3, 1001, (64 << 10) // es):
+            for key, v in rs_a2a(n, 0, dt).items():
+                ok[f"{dt}/{n}/{key}"] = v
+    for op in ("MAX", "MIN"):
+        ok[f"op/{op}"] = rs_a2a(257, 1, op=op)["rs"]
+    ok["algos"] = all(a == "ipc_ll" for a in algos.values()) or algos
+    good = True
+    for k in range(iters):
+        good = all(rs_a2a(1 + (k * 53) % 3000, k).values()) and good
+        z = torch.full((100,), float(rank + k), device=d)
+        dist.broadcast(z, src=k % size)
+        good = good and bool(torch.all(z == k % size + k))
+        dist.all_reduce(z)
+        good = good and bool(torch.all(z == size * (k % size + k)))
+    ok["interleaved"] = good
+    return ok
+
+
 def partial_rows(rank, size, device="cuda", reps=6):
     """2-shot all-reduces whose last row of W tiles is partial (the padding tiles of that row
     are skipped by the pull pipeline), mixed with other sizes so every block's LDS ring holds

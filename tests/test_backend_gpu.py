@@ -357,6 +357,21 @@ def test_shared_gpu_world8():
     for ok in _gpu_launch(W.ll_rooted_probe, 8, args=("cuda", 12), env=env):
         assert ok.pop("algos") is True, ok
         assert all(ok.values()), ok
+    for ok in _gpu_launch(W.ll_exchange_probe, 8, args=("cuda", 8), env=env):
+        algos = ok.pop("algos")  # (list all_to_all: host engine on a shared GPU, see above)
+        assert algos is True or algos.get("rs") == "ipc_ll", algos
+        assert all(ok.values()), ok
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ll_reduce_scatter_all_to_all_on_shared_gpu(world):
+    # small reduce_scatter / all_to_all take the LL exchange kernels (chunk q pushed to rank q)
+    # (the list all_to_all is served by the host engine on a shared GPU; the LL all-to-all kernel is
+    # checked by the LL self-test, which has to pass for reduce_scatter to report ipc_ll)
+    for ok in _gpu_launch(W.ll_exchange_probe, world, env={"PDCC_ALGO": "ipc"}):
+        algos = ok.pop("algos")
+        assert algos is True or algos.get("rs") == "ipc_ll", algos
+        assert all(ok.values()), ok
 
 
 def test_ll_rooted_selftest_gate():

@@ -136,11 +136,14 @@ def test_ll_allreduce_words_are_single_stores_and_uncached_polls(kernels):
     # data with an old epoch or the reverse), and the poll must read 8 bytes at system
     # scope (uncached, past L2); no scratch, flat accesses or calls
     # (and the rooted k_ll_reduce / k_ll_rooted: data one way, token lines on the other pairs)
+    # (and k_ll_reduce_scatter / k_ll_alltoall: chunk q pushed to rank q)
     ks = {n: b for n, b in kernels.items() if any(k in n for k in ("k_ll_allreduce", "k_ll_allgather", "k_ll_reduce",
-                                                                 "k_ll_rooted"))}
+                                                                 "k_ll_rooted", "k_ll_alltoall"))}
     assert sum("k_ll_allgather" in n for n in ks) == 7, sorted(ks)  # all-gather: one per W = 2..8
     assert sum("k_ll_rooted" in n for n in ks) == 7, sorted(ks)  # broadcast / gather / scatter: one per W
-    assert sum("k_ll_reduce" in n for n in ks) >= 7, sorted(ks)
+    assert sum("11k_ll_reduceI" in n for n in ks) >= 7, sorted(ks)  # (mangled: not k_ll_reduce_scatter)
+    assert sum("k_ll_reduce_scatter" in n for n in ks) >= 7, sorted(ks)
+    assert sum("k_ll_alltoall" in n for n in ks) == 7, sorted(ks)
     assert len(ks) >= 28, sorted(kernels)[:20]
     for name, body in ks.items():
         stores = [s for s in body if s.startswith("global_store_dwordx2") and s.endswith("sc0 sc1")]

@@ -150,6 +150,14 @@ def test_ll_rooted_distinct_gpus(world):
         assert all(ok.values()), ok
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_ll_reduce_scatter_all_to_all_distinct_gpus(world):
+    for ok in _run(W.ll_exchange_probe, world, env={"PDCC_ALGO": "ipc"}):
+        algos = ok.pop("algos")
+        assert algos is True or algos.get("rs") == "ipc_ll", algos
+        assert all(ok.values()), ok
+
+
 @pytest.mark.parametrize("algo", ["rccl", "ipc", "auto"])
 def test_sync_collective_after_async_distinct_gpus(algo):
     for ok in _run(W.async_then_sync, 2, env={"PDCC_ALGO": algo}):
