@@ -160,6 +160,9 @@ def run_rank(args):
     numel = args.bytes // 4
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.rand(numel, device=dev, generator=gen).mul_(1e-3)
+    # in-place SUM multiplies the data by W per step (+inf after ~43 steps at W=8): every
+    # phase starts from this copy again (restored outside the timed regions)
+    x0 = x.clone()
 
     def sync():
         dist.barrier()
@@ -173,6 +176,7 @@ def run_rank(args):
 
     for _ in range(args.warmup):
         dist.all_reduce(x)
+    x.copy_(x0)
     sync()
     if rank == 0:
         print(f"[bench] world={world} warm-up done, timing {args.steps} steps", file=sys.stderr, flush=True)
@@ -180,23 +184,27 @@ def run_rank(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         dist.all_reduce(x)
+    algo = native.last_algo() or "?"  # the engine that served the timed steps
     csync()
     dist.barrier()
     csync()
     total = max_over_ranks(time.perf_counter() - t0)
-    ar = {k: v[0] for k, v in native.stats().items() if k.startswith("allreduce/")}
-    algo = max(ar, key=ar.get).split("/", 1)[1] if ar else "?"
+    finite = bool(torch.isfinite(x).all().item())
     ms_per_step = total / args.steps * 1e3
 
     # ---- p50 of individually bracketed steps (BASELINE.md method)
     lat = []
     for _ in range(args.steps):
+        x.copy_(x0)
         sync()
         s0 = time.perf_counter()
         dist.all_reduce(x)
         csync()
         lat.append(max_over_ranks(time.perf_counter() - s0))
     p50 = statistics.median(lat)
+    finite = finite and bool(torch.isfinite(x).all().item())
+    x.copy_(x0)
+    del x0
 
     # ---- correctness of the headline path
     y = torch.full((numel,), float(rank + 1), device=dev)
@@ -239,6 +247,7 @@ def run_rank(args):
                 "device": dev.type,
             },
             "correct": correct,
+            "data_finite": finite,
             "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
             "extras": extras,
         }
@@ -257,14 +266,29 @@ def run_rank(args):
         os._exit(0)
 
     extras = {}
-    if args.extras and on_gpu:
+    if args.extras:
         timer = threading.Timer(float(os.environ.get("PDCC_BENCH_EXTRAS_S", "240")), deadline, args=("extras",))
         timer.daemon = True
         timer.start()
+        # the conformance pass first: on the driver's multi-GPU node this is the first
+        # distinct-GPU run of every engine, so its verdict must not wait behind the sweeps
         try:
-            extras = run_extras(world, rank, dev, native, x)
-        except Exception as e:  # extras never break the headline line
-            extras = {"error": f"{type(e).__name__}: {e}"[:500]}
+            from pytorch_distributed_collective_communication_amd.utils import conformance
+
+            progress("conformance pass")
+            EXTRAS_PARTIAL["conformance"] = conformance.run(
+                rank, world, dev, deadline_s=float(os.environ.get("PDCC_BENCH_CONFORMANCE_S", "45")),
+                max_bytes=(64 << 20) if on_gpu and not SMALL else (1 << 20))
+        except Exception as e:
+            EXTRAS_PARTIAL["conformance"] = {"all_ok": False, "error": f"{type(e).__name__}: {e}"[:500]}
+        if on_gpu:
+            try:
+                extras = run_extras(world, rank, dev, native, x)
+            except Exception as e:  # extras never break the headline line
+                extras = dict(EXTRAS_PARTIAL)
+                extras["error"] = f"{type(e).__name__}: {e}"[:500]
+        else:
+            extras = dict(EXTRAS_PARTIAL)
         timer.cancel()
     emit(extras)
     guard = threading.Timer(60.0, lambda: os._exit(0))  # teardown must not hang the job either
@@ -323,7 +347,11 @@ def run_extras(world, rank, dev, native, x):
         return f.item() > 0
 
     big = (1 << 30) if not SMALL else (64 << 20)
-    for algo in ("rccl", "ipc", "ipc_push"):
+    rccl_ok = "rccl_ok=1" in native.describe()
+    algos = ("rccl", "ipc", "ipc_push") if rccl_ok else ("ipc", "ipc_push")
+    if not rccl_ok:
+        out["rccl_rows"] = "dropped: ranks share a GPU, RCCL unavailable"
+    for algo in algos:
         try:
             gb.set_algo(algo)
             progress(f"algo A/B: {algo}")
@@ -333,8 +361,10 @@ def run_extras(world, rank, dev, native, x):
                 t = x[: nbytes // 4]
                 lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
                 out[f"allreduce_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
+                out[f"allreduce_{algo}_{nbytes}B_engine"] = gb.last_algo()  # what actually ran
                 if nbytes >= (1 << 20):
                     out[f"allreduce_{algo}_{nbytes}B_busbw"] = round(busbw(nbytes, world, lat), 1)
+                t.uniform_(0.0, 1e-3)  # in-place SUM grew it by W per call: fresh finite data
             v = torch.full((1 << 20,), float(rank + 1), device=dev)
             dist.all_reduce(v, group=g)
             good = bool(torch.all(v == world * (world + 1) / 2).item())
@@ -355,6 +385,7 @@ def run_extras(world, rank, dev, native, x):
                 for name, (coll, total, fn) in cases.items():
                     lat = _time_op(fn, 10 if nbytes >= (16 << 20) else 30)
                     out[f"{name}_{algo}_{nbytes}B_us"] = round(lat * 1e6, 1)
+                    out[f"{name}_{algo}_{nbytes}B_engine"] = gb.last_algo()
                     out[f"{name}_{algo}_{nbytes}B_busbw"] = round(bb(coll, total, world, lat), 1)
                 ag_in = torch.full((per,), float(rank), device=dev)
                 dist.all_gather_into_tensor(full, ag_in, group=g)
@@ -451,6 +482,7 @@ def rccl_tuning(world, rank, dev, x):
         g = _group_with_env(world, env)
         t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
         sweep[str(ctas)] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
+        big.uniform_(0.0, 1e-3)  # in-place SUM grew it by W per call: fresh finite data
         dist.destroy_process_group(g)
     res["cta_sweep_allreduce_busbw"] = sweep
     per = ((256 << 20) if not SMALL else (16 << 20)) // 4
@@ -496,6 +528,7 @@ def ipc_grid_sweep(world, rank, dev, x):
             g = _group_with_env(world, {"PDCC_ALGO": algo, "PDCC_IPC_GRID": grid})
             t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
             gsweep[f"{algo}_g{grid}"] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
+            big.uniform_(0.0, 1e-3)
             dist.destroy_process_group(g)
     v = torch.full((1 << 22,), float(rank + 1), device=dev)
     g = _group_with_env(world, {"PDCC_ALGO": "ipc", "PDCC_IPC_GRID": 1024})
@@ -552,8 +585,11 @@ def _p50_coll(fn, iters=5):
     import torch
     import torch.distributed as dist
 
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
     fn()
     lat = []
+    _p50_coll.engine = "?"
     for _ in range(iters):
         dist.barrier()
         torch.cuda.synchronize()
@@ -561,9 +597,16 @@ def _p50_coll(fn, iters=5):
         fn()
         torch.cuda.synchronize()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        try:  # the engine that ran fn (read before the CPU-tensor MAX below records "shm")
+            _p50_coll.engine = be.native_backend(_p50_coll.group, "cuda").last_algo()
+        except Exception:
+            pass
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         lat.append(t.item())
     return statistics.median(lat)
+
+
+_p50_coll.group = None  # the group whose engine _p50_coll reports (None: default group)
 
 
 def baseline_configs(world, rank, dev, x):
@@ -580,13 +623,15 @@ def baseline_configs(world, rank, dev, x):
     def rec(name, coll, total_bytes, fn, iters=5, check=None):
         progress(name)
         t = _p50_coll(fn, iters)
-        res[name] = {"p50_ms": round(t * 1e3, 3), "busbw_GBps": round(bb(coll, total_bytes, world, t), 1)}
+        res[name] = {"p50_ms": round(t * 1e3, 3), "busbw_GBps": round(bb(coll, total_bytes, world, t), 1),
+                     "engine": _p50_coll.engine}
         if check is not None:
             res[name]["correct"] = bool(check())
 
     S = 1 << 30 if not SMALL else 64 << 20
     n = S // 4
     chunk = n // world
+    x.uniform_(0.0, 1e-3)
     rec("all_reduce_1GiB", "all_reduce", S, lambda: dist.all_reduce(x))
     rec("reduce_1GiB", "reduce", S, lambda: dist.reduce(x, dst=0))
     rec("broadcast_1GiB", "broadcast", S, lambda: dist.broadcast(x, src=0))

@@ -118,6 +118,7 @@ Config Config::from_env() {
     else if (v == "staged") c.list_gather_p2p = false;
     else throw std::runtime_error("PDCC_LIST_GATHER must be p2p|staged, got " + v);
   }
+  c.a2a_list_agree = env_bool("PDCC_A2A_LIST_AGREE", c.a2a_list_agree);
   c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
   c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
   c.rccl_wide_ctas = std::max(0, env_int("PDCC_RCCL_WIDE_CTAS", c.rccl_wide_ctas));
@@ -157,6 +158,7 @@ std::string Config::describe() const {
     << " rccl_wide_min=" << rccl_wide_min
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
+    << " a2a_list_agree=" << a2a_list_agree
     << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
     << " watchdog_ms=" << watchdog_ms << " stream=" << (stream_mode == 0 ? "auto" : stream_mode == 1 ? "high" : stream_mode == 2 ? "comm" : "current");

@@ -101,6 +101,10 @@ struct Config {
   // all_gather into a list of separate tensors on RCCL: p2p = grouped ncclSend/Recv straight
   // into the list (zero copy), staged = ncclAllGather into a staging buffer + K2 unpack
   bool list_gather_p2p = true;             // PDCC_LIST_GATHER=p2p|staged
+  // all_to_all with tensor lists: chunk sizes are rank-local, so the ranks agree (one
+  // host-transport round) whether every chunk is equal before taking the IPC/LL/autotuned
+  // engines; 0 = lists always go to grouped point-to-point (no host round per call)
+  bool a2a_list_agree = true;              // PDCC_A2A_LIST_AGREE
   bool world1_local = true;                // PDCC_WORLD1_LOCAL=0: run RCCL even for 1-rank groups (tests)
   bool eager_init = false;                 // PDCC_EAGER_INIT=1: GPU setup at group construction
   // host transport

@@ -941,20 +941,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   const c10::hip::HIPStreamMasqueradingAsCUDA comm = on_current ? cur : (stream ? *stream : ds.stream);
   StreamSync& sy = *ds.sync;
   bool use_sig = false;
-  if (comm == cur && !cap && !stream) {
-    // a synchronous collective after async ones that may still be running on the group's
-    // comm stream: order it behind them (two collectives of one group never overlap; p2p
-    // pair streams are not waited for -- their peers may post the matching op later)
-    std::lock_guard<std::mutex> lk(sy.mu);
-    auto it = sy.comm_done.find(ds.stream.stream());
-    if (it != sy.comm_done.end() && it->second.ptr) {
-      uint64_t& seen = sy.comm_seen[cur.stream()];
-      if (seen < it->second.next) {
-        PDCC_HIP(hipStreamWaitValue64(cur.stream(), it->second.ptr, it->second.next, hipStreamWaitValueGte, ~0ull));
-        seen = it->second.next;
-      }
-    }
-  }
+  // a synchronous collective after async ones that may still be running on the group's
+  // comm stream: order it behind them (two collectives of one group never overlap)
+  if (comm == cur && !cap && !stream) order_after_async(ds, cur.stream());
   SignalWord* done_word = nullptr;
   if (comm != cur) {
     {
@@ -1039,13 +1028,31 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   return w;
 }
 
+// Make stream `s` wait (stream memory op, no host block) for every async collective of
+// this group issued so far on the group's comm stream. p2p pair streams are not waited
+// for: their peers may post the matching op later.
+void ProcessGroupMI355X::order_after_async(DeviceState& ds, hipStream_t s) {
+  StreamSync& sy = *ds.sync;
+  std::lock_guard<std::mutex> lk(sy.mu);
+  auto it = sy.comm_done.find(ds.stream.stream());
+  if (it == sy.comm_done.end() || !it->second.ptr) return;
+  uint64_t& seen = sy.comm_seen[s];
+  if (seen < it->second.next) {
+    PDCC_HIP(hipStreamWaitValue64(s, it->second.ptr, it->second.next, hipStreamWaitValueGte, ~0ull));
+    seen = it->second.next;
+  }
+}
+
 // =================================================================== autotuner
 std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can,
-                                                      bool zc_can) const {
+                                                      bool zc_can, bool ll_can) const {
   std::vector<Algo> v;
   if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || !ipc_can || !same_host_ || coalescing_) return v;
   if ((int)c >= 32 || !(cfg_.autotune_colls & (1u << (int)c))) return v;
   if (bytes < cfg_.autotune_min || bytes > cfg_.autotune_max) return v;
+  // LL sizes keep the static choice: a race there would time the LL kernel and then apply
+  // the verdict to the staged protocol the rest of the power-of-two bucket takes
+  if (ll_can && bytes_in_ll_range(bytes)) return v;
   if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
   else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
   else return {};
@@ -1075,7 +1082,7 @@ Algo ProcessGroupMI355X::tuned(const TuneKey& k) {
 // (topology, dtype/op support, the consensus table), so every rank picks the same.
 Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can,
                                 bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
-  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok);
+  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok, ds.ll_ok);
   if (cands.empty()) return a0;
   const TuneKey key{(int)c, dtype, op, size_bucket(bytes)};
   const Algo t = tuned(key);
@@ -1092,6 +1099,10 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
     if (a == Algo::RCCL_WIDE) rccl_wide(ds);
     if (is_ipc(a)) ipc(ds);
   }
+  // the race runs on the caller's stream: it must not overlap an async collective of this
+  // group still in flight on the comm stream (IPC kernels of one rank share the per-block
+  // counters, the staging buffer and the LL epoch word)
+  order_after_async(ds, current_stream(ds.device));
   return tune(key, cands);
 }
 

@@ -1090,7 +1090,27 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall(std::vector<at::Tens
   TORCH_CHECK((int)outputs.size() == size_ && (int)inputs.size() == size_,
               "ProcessGroupMI355X::alltoall: expects one input and one output tensor per rank");
   before_op(Coll::ALLTOALL, inputs, -1);
-  if (inputs[0].is_cuda()) return gpu_alltoall(outputs, inputs, false, eff_timeout(opts.timeout));
+  if (inputs[0].is_cuda()) {
+    // equal chunks (every input and output of every rank the same byte count) take the
+    // same engines as all_to_all_single with empty splits: IPC / LL / autotuned. Chunk
+    // sizes are rank-local facts here, so the ranks agree first (one host-transport
+    // round of two doubles): a rank with uneven chunks sends everyone to grouped p2p.
+    bool equal = true;
+    const size_t b0 = inputs[0].nbytes();
+    for (int r = 0; r < size_; ++r)
+      equal = equal && inputs[r].nbytes() == b0 && outputs[r].nbytes() == b0 &&
+              inputs[r].scalar_type() == inputs[0].scalar_type() &&
+              outputs[r].scalar_type() == inputs[0].scalar_type();
+    if (size_ > 1 && same_host_ && cfg_.a2a_list_agree) {
+      const double x = equal ? (double)b0 : -1.0;
+      double v[2] = {x, -x};  // MIN -> {min over ranks, -max over ranks}
+      shm().allreduce(v, 2, at::kDouble, c10d::ReduceOp::MIN, eff_timeout(opts.timeout));
+      equal = v[0] >= 0.0 && v[0] == -v[1];
+    } else if (size_ > 1) {
+      equal = false;
+    }
+    return gpu_alltoall(outputs, inputs, equal, eff_timeout(opts.timeout));
+  }
   const auto t0 = std::chrono::steady_clock::now();
   std::vector<at::Tensor> ci;
   std::vector<Contig> co;

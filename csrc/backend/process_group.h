@@ -485,7 +485,10 @@ class ProcessGroupMI355X : public c10d::Backend {
   std::mutex tune_mu_;
   std::atomic<bool> tuning_{false};  // an autotune race is running: IPC spin timeouts are its verdict
   // engines worth timing for this call (reference engine first); empty = no tuning
-  std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can, bool zc_can) const;
+  std::vector<Algo> tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can, bool zc_can,
+                                    bool ll_can) const;
+  // stream `s` waits for every async collective of this group issued so far (comm stream)
+  void order_after_async(DeviceState& ds, hipStream_t s);
   Algo tuned(const TuneKey& k);
   // engine for one call: the static choice `a0`, or the tuned one for this key (tuning now,
   // through `tune(cands)`, when the key has no decision yet)

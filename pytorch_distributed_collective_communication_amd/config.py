@@ -29,6 +29,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_RCCL_SPLIT_SHARE | 1 | ncclCommSplit children share the parent's resources |
 | PDCC_RCCL_BUFFSIZE / _ALGO / _PROTO / _MIN_NCHANNELS / _MAX_NCHANNELS / _NTHREADS / _MSCCL / _MSCCLPP | unset | forwarded to NCCL_* / RCCL_* before the process's first communicator (the user's own NCCL_* setting wins) |
 | PDCC_LIST_GATHER | p2p | all_gather into separate tensors on RCCL: grouped send/recv into the list (p2p) or ring all_gather + K2 unpack (staged) |
+| PDCC_A2A_LIST_AGREE | 1 | GPU ``all_to_all`` with tensor lists: the ranks agree (one host round) whether every chunk is equal, which unlocks the IPC/LL engines; 0: lists always use grouped point-to-point |
 | PDCC_EAGER_INIT | 0 | build topology, IPC self-test and RCCL communicator when the group is created |
 | PDCC_WORLD1_LOCAL | 1 | 1-rank groups short-circuit (0: still call RCCL, for tests) |
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
@@ -96,6 +97,7 @@ class Config:
     rccl_group_comm: str = "share"
     rccl_split_share: bool = True
     list_gather: str = "p2p"
+    a2a_list_agree: bool = True
     eager_init: bool = False
     world1_local: bool = True
     shm_slot_bytes: int = 8 << 20
@@ -121,7 +123,7 @@ _ENV = {
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",
     "rccl_group_comm": "PDCC_RCCL_GROUP_COMM", "rccl_split_share": "PDCC_RCCL_SPLIT_SHARE",
-    "list_gather": "PDCC_LIST_GATHER", "eager_init": "PDCC_EAGER_INIT",
+    "list_gather": "PDCC_LIST_GATHER", "a2a_list_agree": "PDCC_A2A_LIST_AGREE", "eager_init": "PDCC_EAGER_INIT",
     "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",
     "rccl_wide_ctas": "PDCC_RCCL_WIDE_CTAS", "rccl_wide_min": "PDCC_RCCL_WIDE_MIN",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",

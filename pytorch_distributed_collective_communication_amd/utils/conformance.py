@@ -1,0 +1,377 @@
+"""Cross-rank conformance pass of the ``mi355x`` backend, one process per rank.
+
+The reference verifies its six collectives by reading their printed outputs
+(reference main.py:14,23,37,52,68,81; golden values README.md:105-284, SURVEY.md
+§4.2). This module turns those goldens -- plus random-data numerics and the
+protocol-specific paths of this library -- into a bounded pass every rank runs
+together, so the first multi-GPU run of ``bench.py`` (the driver's scaling run)
+is also the first distinct-GPU conformance run. Each check records whether it
+passed on EVERY rank and which engine actually served it (``last_algo()``):
+
+* ``golden/<engine>/...``  -- the reference's own calls, SUM/PRODUCT/MAX/MIN on
+  ``[r+2, 10-r, r]`` for reduce / all_reduce (main.py:14-15, 23-24), scatter of
+  ``[1..W]``, gather / all_gather of ``[rank]``, broadcast of ``[0]``;
+* ``random/<engine>/<coll>/<dtype>/<op>/<bytes>`` -- all_reduce and
+  reduce_scatter of seeded random fp32 / bf16 data against an fp64 torch
+  reduction of ALL ranks' inputs (every rank regenerates them). MAX/MIN must be
+  bitwise; SUM/AVG within ``(W + 1)`` units of the dtype's epsilon times
+  ``sum_r |x_r|`` (engines only differ in summation order and where 16-bit
+  types round); PRODUCT within ``(W + 1)`` eps of ``|prod|``;
+* ``ll/<kind>`` -- all eight LL kinds (flag-tagged pushes) at 4 KiB, with the
+  engine required to be ``ipc_ll`` (the list ``all_to_all`` included);
+* ``zc/<...>`` -- zero-copy pull all-reduce, push all-reduce, flat all-gather,
+  reduce-scatter and 2-shot broadcast at 4 MiB, engine required ``*_zc``;
+* ``async_then_sync/<engine>`` -- an ``async_op=True`` all_reduce immediately
+  followed by a synchronous one on the same tensor;
+* ``shared_comm/<engine>`` -- two groups with the same members (one shared
+  communicator) interleaving async and sync all_reduces (main.py:11,21,... build
+  exactly such groups).
+
+The pass stops early (every rank at the same check) once ``deadline_s`` is spent;
+checks not run are listed under ``skipped``.
+"""
+from __future__ import annotations
+
+import datetime
+import time
+
+_EPS = {"float32": 2.0 ** -23, "bfloat16": 2.0 ** -8, "float16": 2.0 ** -11, "float64": 2.0 ** -52}
+
+
+def _seeded(shape, dtype, seed, dev, lo=-1.0, hi=1.0):
+    import torch
+
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.rand(shape, generator=g, device=dev, dtype=torch.float32)
+    return (x * (hi - lo) + lo).to(dtype)
+
+
+def _close(got, xs, op, world, dtype_name):
+    """`got` (any dtype) vs the op over `xs` (list of every rank's input, same dtype)."""
+    import torch
+
+    if op in ("MAX", "MIN"):
+        st = torch.stack(xs)
+        ref = st.amax(0) if op == "MAX" else st.amin(0)
+        return bool(torch.equal(got, ref))
+    st = torch.stack([x.double() for x in xs])
+    eps = _EPS[dtype_name] * (world + 1)
+    g = got.double()
+    if op == "PRODUCT":
+        ref = st.prod(0)
+        return bool(torch.all((g - ref).abs() <= eps * ref.abs() + 1e-30).item())
+    ref = st.sum(0)
+    bound = st.abs().sum(0)
+    if op == "AVG":
+        ref, bound = ref / world, bound / world
+    return bool(torch.all((g - ref).abs() <= eps * bound + 1e-30).item())
+
+
+class _Pass:
+    def __init__(self, rank, world, dev, deadline_s):
+        self.rank, self.world, self.dev = rank, world, dev
+        self.t0 = time.monotonic()
+        self.t_end = self.t0 + deadline_s
+        self.checks: dict = {}
+        self.skipped: list = []
+        self.stopped = False
+
+    def agree(self, ok: bool) -> tuple[bool, bool]:
+        """(ok on every rank, every rank still inside the deadline): one host round
+        on the default group, so every rank stops at the same check."""
+        import torch
+        import torch.distributed as dist
+
+        v = torch.tensor([1.0 if ok else 0.0, 1.0 if time.monotonic() < self.t_end else 0.0], dtype=torch.float64)
+        if self.world > 1:
+            dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return v[0].item() > 0, v[1].item() > 0
+
+    def check(self, name, gb, fn, expect_engine=None):
+        if self.stopped:
+            self.skipped.append(name)
+            return
+        err = None
+        try:
+            ok = bool(fn())
+        except Exception as e:  # a failing check must not stop the pass on this rank only
+            ok, err = False, f"{type(e).__name__}: {e}"[:200]
+        engine = gb.last_algo() if gb is not None else "?"
+        if expect_engine is not None and not _engine_matches(engine, expect_engine):
+            ok = False
+        all_ok, in_time = self.agree(ok)
+        rec = {"ok": all_ok, "engine": engine}
+        if expect_engine is not None:
+            rec["want"] = expect_engine
+        if err:
+            rec["error"] = err
+        self.checks[name] = rec
+        if not in_time:
+            self.stopped = True
+
+    def result(self):
+        failed = [k for k, v in self.checks.items() if not v["ok"]]
+        return {"all_ok": not failed and not self.skipped, "passed": len(self.checks) - len(failed),
+                "failed": failed, "skipped": self.skipped, "elapsed_s": round(time.monotonic() - self.t0, 2),
+                "checks": self.checks}
+
+
+def _engine_matches(engine: str, want: str) -> bool:
+    if want.endswith("*"):
+        return engine.startswith(want[:-1])
+    return engine == want
+
+
+def run(rank: int, world: int, dev, deadline_s: float = 45.0, max_bytes: int = 64 << 20,
+        engines=None, timeout_s: float = 30.0) -> dict:
+    """Run the pass on every rank of the default group (collective). `dev` is this
+    rank's device (a GPU, or CPU for the host-transport rehearsal)."""
+    import torch
+    import torch.distributed as dist
+
+    from ..parallel import backend as be
+
+    P = _Pass(rank, world, dev, deadline_s)
+    on_gpu = dev.type == "cuda"
+    to = datetime.timedelta(seconds=timeout_s)
+    g = dist.new_group(list(range(world)), timeout=to)
+    g2 = dist.new_group(list(range(world)), timeout=to)  # same members: a shared communicator
+    gb = be.native_backend(g, dev.type)
+    gb2 = be.native_backend(g2, dev.type)
+    # first collective sets up the group's topology (and IPC self-test) on this device
+    warm = torch.zeros(1, device=dev)
+    dist.all_reduce(warm, group=g)
+    dist.all_reduce(warm, group=g2)
+    desc = gb.describe()
+    rccl_ok = "rccl_ok=1" in desc
+    ipc_ok = "ipc_ok=1" in desc
+    zc_ok = "zc_ok=1" in desc
+    ll_ok = "ll_ok=1" in desc
+    info = {"world": world, "device": dev.type, "rccl_ok": rccl_ok, "ipc_ok": ipc_ok, "zc_ok": zc_ok, "ll_ok": ll_ok}
+    if engines is None:
+        if not on_gpu or world == 1:
+            engines = ["auto"]
+        else:
+            engines = (["rccl"] if rccl_ok else []) + (["ipc"] if ipc_ok else []) + ["auto"]
+    if on_gpu and world > 1 and not rccl_ok:
+        info["rccl_skipped"] = "ranks share a GPU: RCCL refuses duplicate devices"
+    W = world
+    f32 = torch.float32
+
+    def set_engine(e):
+        if hasattr(gb, "set_algo"):
+            gb.set_algo(e)
+            gb2.set_algo(e)
+
+    for eng in engines:
+        set_engine(eng)
+        # ---- golden table, the reference's shapes
+        for op in ("SUM", "PRODUCT", "MAX", "MIN"):
+            rop = getattr(dist.ReduceOp, op)
+            vals = [[r + 2, 10 - r, r] for r in range(W)]
+
+            def ar(op=op, rop=rop, vals=vals):
+                t = torch.tensor(vals[rank], dtype=f32, device=dev)
+                dist.all_reduce(t, op=rop, group=g)
+                return _close(t.cpu(), [torch.tensor(v, dtype=f32) for v in vals], op, W, "float32")
+
+            def rd(op=op, rop=rop, vals=vals):
+                t = torch.tensor(vals[rank], dtype=f32, device=dev)
+                dist.reduce(t, dst=0, op=rop, group=g)
+                if rank != 0:  # non-root buffers are left untouched
+                    return t.cpu().tolist() == [float(v) for v in vals[rank]]
+                return _close(t.cpu(), [torch.tensor(v, dtype=f32) for v in vals], op, W, "float32")
+
+            P.check(f"golden/{eng}/all_reduce/{op}", gb, ar)
+            P.check(f"golden/{eng}/reduce/{op}", gb, rd)
+
+        def scatter():
+            t = torch.empty(1, device=dev)
+            lst = [torch.tensor([i + 1.0], device=dev) for i in range(W)] if rank == 0 else []
+            dist.scatter(t, scatter_list=lst, src=0, group=g)
+            return t.item() == rank + 1.0
+
+        def gather():
+            t = torch.tensor([float(rank)], device=dev)
+            lst = [torch.empty(1, device=dev) for _ in range(W)] if rank == 0 else []
+            dist.gather(t, gather_list=lst, dst=0, group=g)
+            return rank != 0 or [x.item() for x in lst] == [float(r) for r in range(W)]
+
+        def all_gather():
+            lst = [torch.empty(1, device=dev) for _ in range(W)]
+            dist.all_gather(lst, torch.tensor([float(rank)], device=dev), group=g)
+            return [x.item() for x in lst] == [float(r) for r in range(W)]
+
+        def broadcast():
+            t = torch.tensor([0.0], device=dev) if rank == 0 else torch.full((1,), -7.0, device=dev)
+            dist.broadcast(t, src=0, group=g)
+            return t.item() == 0.0
+
+        for name, fn in (("scatter", scatter), ("gather", gather), ("all_gather", all_gather),
+                         ("broadcast", broadcast)):
+            P.check(f"golden/{eng}/{name}", gb, fn)
+
+        # ---- random data vs an fp64 reduction of every rank's seeded input
+        sizes = [s for s in (4, 64 << 10, 1 << 20, 64 << 20) if s <= max_bytes]
+        for dtn in ("float32", "bfloat16"):
+            dt = getattr(torch, dtn)
+            es = torch.tensor([], dtype=dt).element_size()
+            for nbytes in sizes:
+                n = max(1, nbytes // es)
+                seed = 1000 * nbytes + (17 if dtn == "bfloat16" else 0)
+
+                def ar_rand(n=n, dt=dt, dtn=dtn, seed=seed):
+                    xs = [_seeded((n,), dt, seed + r, dev) for r in range(W)]
+                    t = xs[rank].clone()
+                    dist.all_reduce(t, group=g)
+                    return _close(t, xs, "SUM", W, dtn)
+
+                def rs_rand(n=n, dt=dt, dtn=dtn, seed=seed):
+                    m = max(1, n // W)
+                    xs = [_seeded((m * W,), dt, seed + 7 + r, dev) for r in range(W)]
+                    out = torch.empty(m, dtype=dt, device=dev)
+                    dist.reduce_scatter_tensor(out, xs[rank].clone(), group=g)
+                    return _close(out, [x[rank * m:(rank + 1) * m] for x in xs], "SUM", W, dtn)
+
+                P.check(f"random/{eng}/all_reduce/{dtn}/SUM/{nbytes}", gb, ar_rand)
+                P.check(f"random/{eng}/reduce_scatter/{dtn}/SUM/{nbytes}", gb, rs_rand)
+        for op in ("AVG", "PRODUCT", "MAX", "MIN"):
+            n = (64 << 10) // 4
+            lo, hi = (0.9, 1.1) if op == "PRODUCT" else (-1.0, 1.0)
+
+            def ar_op(op=op, n=n, lo=lo, hi=hi):
+                xs = [_seeded((n,), f32, 99 + r, dev, lo, hi) for r in range(W)]
+                t = xs[rank].clone()
+                dist.all_reduce(t, op=getattr(dist.ReduceOp, op), group=g)
+                return _close(t, xs, op, W, "float32")
+
+            P.check(f"random/{eng}/all_reduce/float32/{op}/{n * 4}", gb, ar_op)
+
+        # ---- async then sync on one tensor, and two same-member groups interleaved
+        def async_then_sync():
+            n = (1 << 20) // 4 if max_bytes >= (1 << 20) else 1024
+            x = torch.full((n,), float(rank + 1), device=dev)
+            w = dist.all_reduce(x, group=g, async_op=True)
+            dist.all_reduce(x, group=g)
+            w.wait()
+            return bool(torch.all(x == W * (W + 1) / 2 * W).item())
+
+        def shared_comm():
+            n = 4096
+            a = [torch.full((n,), float(rank + 1 + 10 * i), device=dev) for i in range(3)]
+            b = [torch.full((n,), float(rank + 1 + 10 * i), device=dev) for i in range(3)]
+            ws = []
+            for i in range(3):
+                ws.append(dist.all_reduce(a[i], group=g, async_op=True))
+                dist.all_reduce(b[i], group=g2)
+            for w in ws:
+                w.wait()
+            want = [W * (W + 1) / 2 + 10 * i * W for i in range(3)]
+            return all(bool(torch.all(a[i] == want[i]).item()) and bool(torch.all(b[i] == want[i]).item())
+                       for i in range(3))
+
+        P.check(f"async_then_sync/{eng}", gb, async_then_sync)
+        P.check(f"shared_comm/{eng}", gb2, shared_comm)
+
+    # ---- protocol-specific paths of the peer-memory engine
+    if on_gpu and world > 1 and ipc_ok:
+        set_engine("ipc")
+        if ll_ok:
+            n = 1024  # 4 KiB of fp32
+            root = W - 1
+
+            def ll_all_reduce():
+                xs = [_seeded((n,), f32, 500 + r, dev) for r in range(W)]
+                t = xs[rank].clone()
+                dist.all_reduce(t, group=g)
+                return _close(t, xs, "SUM", W, "float32")
+
+            def ll_reduce():
+                xs = [_seeded((n,), f32, 600 + r, dev) for r in range(W)]
+                t = xs[rank].clone()
+                dist.reduce(t, dst=root, group=g)
+                return _close(t, xs, "SUM", W, "float32") if rank == root else bool(torch.equal(t, xs[rank]))
+
+            def ll_broadcast():
+                src = _seeded((n,), f32, 700, dev)
+                t = src.clone() if rank == root else torch.zeros(n, device=dev)
+                dist.broadcast(t, src=root, group=g)
+                return bool(torch.equal(t, src))
+
+            def ll_all_gather():
+                xs = [_seeded((n,), f32, 800 + r, dev) for r in range(W)]
+                lst = [torch.empty(n, device=dev) for _ in range(W)]
+                dist.all_gather(lst, xs[rank], group=g)
+                return all(bool(torch.equal(lst[r], xs[r])) for r in range(W))
+
+            def ll_gather():
+                xs = [_seeded((n,), f32, 900 + r, dev) for r in range(W)]
+                lst = [torch.empty(n, device=dev) for _ in range(W)] if rank == 0 else []
+                dist.gather(xs[rank], gather_list=lst, dst=0, group=g)
+                return rank != 0 or all(bool(torch.equal(lst[r], xs[r])) for r in range(W))
+
+            def ll_scatter():
+                xs = [_seeded((n,), f32, 1000 + r, dev) for r in range(W)]
+                t = torch.empty(n, device=dev)
+                dist.scatter(t, scatter_list=xs if rank == 0 else [], src=0, group=g)
+                return bool(torch.equal(t, xs[rank]))
+
+            def ll_reduce_scatter():
+                xs = [[_seeded((n,), f32, 1100 + 10 * r + q, dev) for q in range(W)] for r in range(W)]
+                out = torch.empty(n, device=dev)
+                dist.reduce_scatter(out, [x.clone() for x in xs[rank]], group=g)
+                return _close(out, [xs[r][rank] for r in range(W)], "SUM", W, "float32")
+
+            def ll_all_to_all():
+                xs = [[_seeded((n,), f32, 1200 + 10 * r + q, dev) for q in range(W)] for r in range(W)]
+                outs = [torch.empty(n, device=dev) for _ in range(W)]
+                dist.all_to_all(outs, xs[rank], group=g)
+                return all(bool(torch.equal(outs[q], xs[q][rank])) for q in range(W))
+
+            for name, fn in (("all_reduce", ll_all_reduce), ("reduce", ll_reduce), ("broadcast", ll_broadcast),
+                             ("all_gather", ll_all_gather), ("gather", ll_gather), ("scatter", ll_scatter),
+                             ("reduce_scatter", ll_reduce_scatter), ("all_to_all_list", ll_all_to_all)):
+                P.check(f"ll/{name}", gb, fn, expect_engine="ipc_ll")
+        if zc_ok and max_bytes >= (4 << 20):
+            n = (4 << 20) // 4
+
+            def zc_all_reduce():
+                xs = [_seeded((n,), f32, 1300 + r, dev) for r in range(W)]
+                t = xs[rank].clone()
+                dist.all_reduce(t, group=g)
+                return _close(t, xs, "SUM", W, "float32")
+
+            def zc_all_gather():
+                xs = [_seeded((n // W,), f32, 1400 + r, dev) for r in range(W)]
+                out = torch.empty(n // W * W, device=dev)
+                dist.all_gather_into_tensor(out, xs[rank], group=g)
+                return bool(torch.equal(out, torch.cat(xs)))
+
+            def zc_reduce_scatter():
+                xs = [_seeded((n,), f32, 1500 + r, dev) for r in range(W)]
+                m = n // W
+                out = torch.empty(m, device=dev)
+                dist.reduce_scatter_tensor(out, xs[rank], group=g)
+                return _close(out, [x[rank * m:(rank + 1) * m] for x in xs], "SUM", W, "float32")
+
+            def zc_broadcast():
+                src = _seeded((n,), f32, 1600, dev)
+                t = src.clone() if rank == 0 else torch.zeros(n, device=dev)
+                dist.broadcast(t, src=0, group=g)
+                return bool(torch.equal(t, src))
+
+            P.check("zc/all_reduce_pull", gb, zc_all_reduce, expect_engine="ipc_2shot_zc")
+            P.check("zc/all_gather", gb, zc_all_gather, expect_engine="ipc_zc")
+            P.check("zc/reduce_scatter", gb, zc_reduce_scatter, expect_engine="ipc_zc")
+            P.check("zc/broadcast", gb, zc_broadcast, expect_engine="ipc_2shot_zc")
+            set_engine("ipc_push")
+            P.check("zc/all_reduce_push", gb, zc_all_reduce, expect_engine="ipc_push_zc")
+    set_engine("auto")
+    out = P.result()
+    out["info"] = info
+    for grp in (g2, g):
+        try:
+            dist.destroy_process_group(grp)
+        except Exception:
+            pass
+    return out

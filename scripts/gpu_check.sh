@@ -49,6 +49,8 @@ for s in "$@"; do
         -d "$0/gpurun_out/prof_zc" -o zc -- python3 "$0/scripts/zc_bench.py" --sizes 64M --iters 8 --modes zc' "$(pwd)" ;;
     stgprof) step stgprof 500 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$0/gpurun_out/prof_stg" -o stg -- python3 "$0/scripts/zc_bench.py" --sizes 64M --iters 8 --modes staged' "$(pwd)" ;;
+    conf) step conf 900 python -u -m pytest tests/test_backend_gpu.py -x -v --timeout 300 --timeout-method thread \
+        -k "conformance or list_all_to_all or ll_reduce_scatter or world8 or async or autotune" ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;

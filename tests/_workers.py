@@ -452,7 +452,8 @@ def autotune_probe(rank, size, device="cuda"):
     d = _dev(device)
     ok = []
     for dt in (torch.float32, torch.bfloat16):
-        for n in (16 << 10, 1 << 18, 1 << 20, 4 << 20):
+        # (16 K + 64) fp32 elements: just above the LL range, the smallest tuned bucket
+        for n in ((16 << 10) + 64, 1 << 18, 1 << 20, 4 << 20):
             x = (torch.arange(n, device=d) % 13).to(dt) + rank
             exp = ((torch.arange(n, device=d) % 13).float() * size + size * (size - 1) / 2)
             for _ in range(3):
@@ -1308,3 +1309,37 @@ def async_then_sync(rank, size, device="cuda", rounds=6):
         ok.append(bool(torch.all(big == tri + size * k)) and bool(torch.all(mid == tri + 2 * size * k))
                   and bool(torch.all(small == tri + 3 * size * k)))
     return ok
+
+
+def a2a_list_routing(rank, size, device="cuda"):
+    """dist.all_to_all with tensor lists: equal chunks agree group-wide and take the IPC
+    engines (LL <= 64 KiB, staged IPC at 1 MiB); one rank with an uneven chunk sends every
+    rank to the generic path. Values checked in every case."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    res = {}
+    for tag, n in (("ll", 1000), ("ipc", (1 << 20) // 4)):
+        ins = [torch.full((n,), float(100 * rank + q), device=d) for q in range(size)]
+        outs = [torch.full((n,), -1.0, device=d) for _ in range(size)]
+        dist.all_to_all(outs, ins)
+        res[tag] = (b.last_algo(), all(bool(torch.all(t == 100 * q + rank)) for q, t in enumerate(outs)))
+    # uneven: rank 0 keeps a larger chunk for itself (its self-chunk only), everything else equal
+    n = 1000
+    sizes_in = [2 * n if (rank == 0 and q == 0) else n for q in range(size)]
+    ins = [torch.full((sizes_in[q],), float(100 * rank + q), device=d) for q in range(size)]
+    outs = [torch.full((2 * n if (rank == 0 and q == 0) else n,), -1.0, device=d) for q in range(size)]
+    dist.all_to_all(outs, ins)
+    res["uneven"] = (b.last_algo(), all(bool(torch.all(t == 100 * q + rank)) for q, t in enumerate(outs)))
+    return res
+
+
+def conformance_probe(rank, size, device="cuda", max_bytes=64 << 20):
+    """The bench's conformance pass (utils/conformance.py) run as a test."""
+    from pytorch_distributed_collective_communication_amd.utils import conformance
+
+    return conformance.run(rank, size, _dev(device), deadline_s=120.0, max_bytes=max_bytes)

@@ -34,8 +34,16 @@ def test_bench_self_launch_prints_one_line(n):
     assert rec["correct"] is True
     assert rec["config"]["parallelism"] == f"dp{n}"
     assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    assert rec["data_finite"] is True  # x is restored between phases (no +inf at large W)
+    assert rec["config"]["algo"] == "shm"  # the engine that actually served the timed steps
     if n > 1:
         assert rec["value"] > 0 and rec["vs_baseline"] is not None
+    conf = rec["extras"]["conformance"]
+    assert conf["all_ok"] is True, conf
+    assert not conf["skipped"] and conf["passed"] >= 30
+    for name, c in conf["checks"].items():
+        assert c["engine"] == "shm", (name, c)
+    assert "golden/auto/reduce/PRODUCT" in conf["checks"] and "shared_comm/auto" in conf["checks"]
 
 
 def test_bench_failing_rank_propagates():

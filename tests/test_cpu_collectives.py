@@ -125,3 +125,12 @@ def test_object_collectives():
         assert got["gather_object"] == ([("g", q) for q in range(3)] if r == 0 else None)
         assert got["scatter_object_list"] == ("s", r)
 
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_conformance_pass_host_transport(world):
+    # the bench's conformance pass on CPU tensors (host transport): every check on every rank
+    res = launch(W.conformance_probe, world, args=("cpu", 1 << 20))
+    for r in res:
+        assert r["all_ok"], r
+        assert r["passed"] >= 30 and all(c["engine"] == "shm" for c in r["checks"].values())
