@@ -393,6 +393,7 @@ RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
     if (agree) {
       if (cfg_.group_comm == 1) {
         c = parent;
+        c->add_user();  // from now on its issue order is enforced across streams (RcclComm::enter)
         how = "share";
       } else {
         c = std::make_shared<RcclComm>(*parent, rank_, rccl_opts());
@@ -1293,6 +1294,7 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
   } else if (is_rccl(a)) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
     RcclComm& rc = a == Algo::RCCL_WIDE ? rccl_wide(ds) : rccl(ds);
+    RcclComm::Issue og(rc, s, capturing(s));
     if (rooted) PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
     else PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
   } else {  // HOST, synchronous
@@ -1327,7 +1329,9 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
     else
       ipc_chunked(ic, c, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
-    PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rccl(ds).get(), s));
+    RcclComm& rc = rccl(ds);
+    RcclComm::Issue og(rc, s, capturing(s));
+    PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rc.get(), s));
   } else {
     PDCC_HIP(hipStreamSynchronize(s));
     at::Tensor h = w.cpu();
@@ -1360,6 +1364,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
     ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.max_staging(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
+    RcclComm::Issue og(rc, s, capturing(s));
     if (!rooted && is_flat(wo, bytes)) {
       PDCC_NCCL(ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc.get(), s));
     } else if (!rooted && !cfg_.list_gather_p2p) {
@@ -1425,6 +1430,7 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
     ipc_run(ds, c, z, rank_ == root ? bytes * size_ : 0, kern::kTileBytes, ic.max_staging() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
+    RcclComm::Issue og(rc, s, capturing(s));
     PDCC_NCCL(ncclGroupStart());
     if (rank_ == root) {
       for (int r = 0; r < size_; ++r)
@@ -1489,6 +1495,7 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
       multi_copy_or_memcpy(d, s);
       src = stg.data_ptr();
     }
+    RcclComm::Issue og(rc, s, capturing(s));
     PDCC_NCCL(ncclReduceScatter(src, wo.data_ptr(), wo.numel(), nd, no, rc.get(), s));
   } else {
     PDCC_HIP(hipStreamSynchronize(s));
@@ -1528,6 +1535,7 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
             ic.max_staging() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
+    RcclComm::Issue og(rc, s, capturing(s));
     const size_t chunk = wi[0].nbytes();
     if (equal && is_flat(wi, chunk) && is_flat(wo, chunk)) {
       PDCC_NCCL(ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc.get(), s));
@@ -2073,6 +2081,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::endCoalescing() {
   coalesced_ds_ = nullptr;
   return gpu_run(Coll::SEND, *ds, keep, {}, timeout_, [&](hipStream_t s) {
     if (fns.empty()) return;
+    // the batch runs on the group's communicator (rccl() made it when the first op was posted)
+    RcclComm::Issue og(*ds->rccl, s, capturing(s));
     PDCC_NCCL(ncclGroupStart());
     for (auto& f : fns) f(s);
     PDCC_NCCL(ncclGroupEnd());

@@ -597,6 +597,8 @@ std::string ProcessGroupMI355X::describe() {
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
       << ", zc_ok=" << kv.second->zc_ok << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
       << ", rccl=" << (kv.second->rccl != nullptr) << ", ipc=" << (kv.second->ipc != nullptr)
+      << ", rccl_users=" << (kv.second->rccl ? kv.second->rccl->order().users() : 0)
+      << ", rccl_issue_waits=" << (kv.second->rccl ? kv.second->rccl->order().waits() : 0)
       << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0) << "}";
   o << ")";

@@ -203,6 +203,18 @@ PYBIND11_MODULE(_C, m) {
       // to a device (see supportsSplitting in process_group.h): nothing to do here
       .def("perform_nocolor_split", [](pdcc::ProcessGroupMI355X&, const at::Device&) {});
 
+  // the cross-stream issue order of one RCCL communicator (csrc/device/issue_order.h), exposed
+  // for tests: dry=True logs the stream operations instead of issuing them (no GPU needed)
+  py::class_<pdcc::IssueOrder>(m, "IssueOrder")
+      .def(py::init<bool>(), py::arg("dry") = false)
+      .def("enter", [](pdcc::IssueOrder& o, uintptr_t s) { o.enter(reinterpret_cast<hipStream_t>(s)); })
+      .def("leave", [](pdcc::IssueOrder& o, uintptr_t s) { o.leave(reinterpret_cast<hipStream_t>(s)); })
+      .def("add_user", &pdcc::IssueOrder::add_user)
+      .def("users", &pdcc::IssueOrder::users)
+      .def("ticks", &pdcc::IssueOrder::ticks)
+      .def("waits", &pdcc::IssueOrder::waits)
+      .def("log", &pdcc::IssueOrder::log);
+
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
         py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,

@@ -19,8 +19,11 @@
 
 #include <atomic>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
+
+#include "issue_order.h"
 
 namespace pdcc {
 
@@ -71,7 +74,29 @@ class RcclComm {
   // the split vote compares it so all ranks derive their child from the same parent
   std::string tag;
 
+  // Issue order (see IssueOrder): groups with the same members share one communicator
+  // (PDCC_RCCL_GROUP_COMM=share) and enqueue on different streams; every RCCL enqueue is
+  // bracketed by enter(s) / leave(s) so the ops of this communicator execute in issue order.
+  IssueOrder& order() { return order_; }
+  void add_user() { order_.add_user(); }
+
+  // RAII enter/leave around the RCCL calls of one collective (skipped while capturing)
+  struct Issue {
+    IssueOrder* o;
+    hipStream_t s;
+    Issue(RcclComm& comm, hipStream_t st, bool capturing) : o(capturing ? nullptr : &comm.order_), s(st) {
+      if (o) o->enter(s);
+    }
+    ~Issue() {
+      if (o) o->leave(s);
+    }
+    Issue(const Issue&) = delete;
+    Issue& operator=(const Issue&) = delete;
+  };
+
  private:
+  IssueOrder order_;
+
   ncclComm_t comm_ = nullptr;
   int device_;
   int world_;

@@ -147,3 +147,30 @@ def test_kernel_errors_are_loud():
         ops.reduce_nway([a.float(), a.float()], op="band")
     with pytest.raises(ValueError):
         ops.reduce_nway([a], op="nope")
+
+
+def test_issue_order_across_streams():
+    # two streams, one communicator's issue order: the op on stream B must see stream A's
+    # earlier op even though A is held back by a long sleep kernel
+    import pytorch_distributed_collective_communication_amd as pdcc
+
+    C = pdcc._load_native()
+    for shared in (False, True):
+        o = C.IssueOrder(dry=False)
+        if shared:
+            o.add_user()
+        a, b = torch.cuda.Stream(), torch.cuda.Stream()
+        x = torch.zeros(1 << 20, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(a):
+            o.enter(a.cuda_stream)
+            torch.cuda._sleep(50_000_000)
+            x.fill_(1.0)
+            o.leave(a.cuda_stream)
+        with torch.cuda.stream(b):
+            o.enter(b.cuda_stream)
+            y = x.clone()
+            o.leave(b.cuda_stream)
+        torch.cuda.synchronize()
+        assert bool(torch.all(y == 1.0)), shared
+        assert o.waits() == 1

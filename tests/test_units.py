@@ -131,3 +131,26 @@ def test_python_config_mirror_matches_the_backend(env):
         want = py[key]
         got = cpp[key].rstrip(",)")
         assert got == (str(int(want)) if isinstance(want, bool) else str(want)), (key, got, want)
+
+
+def test_issue_order_bookkeeping_dry():
+    # RcclComm's cross-stream issue order (csrc/device/issue_order.h) without a GPU: the stream
+    # operations it would issue, for one group (lazy ticks) and after a second group shares it
+    import pytorch_distributed_collective_communication_amd as pdcc
+
+    C = pdcc._load_native()
+    o = C.IssueOrder(dry=True)
+    for s in (1, 1):  # same stream: FIFO already, nothing to issue
+        o.enter(s)
+        o.leave(s)
+    assert o.log() == [] and o.waits() == 0
+    o.enter(2)  # switch: tick the previous stream lazily, wait for it
+    o.leave(2)
+    assert o.log() == ["write 1 1", "wait 2 1"] and o.waits() == 1
+    o.add_user()  # shared: every op ticks right after itself
+    o.enter(2)
+    o.leave(2)
+    o.enter(1)
+    o.leave(1)
+    assert o.log()[2:] == ["write 2 2", "wait 1 2", "write 1 3"], o.log()
+    assert o.users() == 2 and o.ticks() == 3 and o.waits() == 2
