@@ -41,6 +41,9 @@ struct Config {
   // no staging copy and no barrier (0 = off; gated by its own self-test).
   size_t ipc_ll_max = 64u << 10;           // PDCC_IPC_LL_MAX
   size_t ipc_zc_cache = 16;                // PDCC_IPC_ZC_CACHE
+  // Zero-copy calls exchange their records on a per-device launcher thread (IpcLauncher in
+  // process_group.h): the caller's host never waits for its peers (0 = inline exchange)
+  bool ipc_zc_async = true;                // PDCC_IPC_ZC_ASYNC
   // Before a group first uses a device, every rank runs the IPC protocol once on known data (1-shot
   // and 2-shot all-reduce, all-gather) with a short spin timeout and checks the results; one failure
   // on any rank (handle open error, timeout, wrong data) disables IPC for the whole group, so a

@@ -255,6 +255,7 @@ DeviceState& ProcessGroupMI355X::dev_local_idx(int d) {
   auto ds = std::make_unique<DeviceState>(
       c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
   ds->device = d;
+  (void)ds->sync->prealloc();  // signal words for stream hand-offs (see StreamSync::alloc)
   // this rank's device record, for point-to-point peers (non-blocking: set only; a
   // peer reads it after posting its own, so a ring of first ops cannot wait in a cycle)
   store_->set("pdcc/devrec/" + std::to_string(rank_), [&] {
@@ -856,10 +857,10 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
       TORCH_CHECK(v[r].size() == sizeof(IpcComm::ZcRec), "pdcc: malformed zero-copy record");
       std::memcpy(&all[r], v[r].data(), sizeof(IpcComm::ZcRec));
     }
-  } else {
+  } else {  // (a launcher job exchanges on the launcher's own channel)
     std::vector<void*> outs;
     for (auto& r : all) outs.push_back(&r);
-    shm().allgather(&mine, outs, sizeof(mine), timeout_);
+    (tls_xchg ? *tls_xchg : shm()).allgather(&mine, outs, sizeof(mine), timeout_);
   }
   bool all_ok = true, fresh = false;
   for (const auto& r : all) {
@@ -875,7 +876,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
       for (const auto& x : v) ok = ok && !x.empty() && x[0] == 1;
     } else {
       double f = ok ? 1.0 : 0.0;
-      shm().allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
+      (tls_xchg ? *tls_xchg : shm()).allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
       ok = f > 0.0;
     }
   }
@@ -904,9 +905,12 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
 void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                                  size_t per_call_max, hipStream_t s, const char* selftest) {
   const size_t body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
-  {
+  if (!tls_xchg) {  // (a launcher job: the caller already recorded the call as zero-copy)
     std::lock_guard<std::mutex> lk(stats_mu_);
     zc_ran_ = body > 0;
+  } else if (body == 0 && ds.launcher) {
+    std::lock_guard<std::mutex> lk(ds.launcher->mu);
+    ++ds.launcher->fallbacks;  // recorded as zero-copy, ran staged (a rank could not export)
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;
@@ -1044,6 +1048,15 @@ void ProcessGroupMI355X::order_after_async(DeviceState& ds, hipStream_t s) {
   }
 }
 
+// A call handed to the IPC launcher runs its zero-copy exchange later, on the launcher's
+// thread: it is recorded as zero-copy now (a rank that cannot export makes it fall back to
+// staging; the launcher counts those, describe() "zc_fallbacks")
+void ProcessGroupMI355X::note_zc(bool exchanges) {
+  if (!exchanges || !cfg_.ipc_zc_async) return;
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  zc_ran_ = true;
+}
+
 // =================================================================== autotuner
 std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can,
                                                       bool zc_can, bool ll_can) const {
@@ -1101,9 +1114,10 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
     if (is_ipc(a)) ipc(ds);
   }
   // the race runs on the caller's stream: it must not overlap an async collective of this
-  // group still in flight on the comm stream (IPC kernels of one rank share the per-block
-  // counters, the staging buffer and the LL epoch word)
+  // group still in flight on the comm stream or the IPC launcher's stream (IPC kernels of
+  // one rank share the per-block counters, the staging buffer and the LL epoch word)
   order_after_async(ds, current_stream(ds.device));
+  launcher_quiesce(ds, current_stream(ds.device));
   return tune(key, cands);
 }
 
@@ -1616,10 +1630,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     icp = ds.ipc;
   }
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
+  const bool zx = zc_exchanges(ds, a, cname, bytes);
   auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, ds, s, to);
-    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, t = t](hipStream_t x) mutable {
+      enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, *dsp, x, to);
+      if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+    });
   }, icp);
+  note_zc(zx);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
                              : one_shot                         ? "ipc_1shot"
@@ -1664,10 +1682,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     icp = ds.ipc;
   }
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
+  const bool zx = zc_exchanges(ds, a, Coll::BROADCAST, bytes);
   auto work = gpu_run(Coll::BROADCAST, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    enqueue_broadcast(a, w, root, ds, s, to);
-    if (!w.is_same(t) && rank_ != root) t.copy_(w);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, t = t](hipStream_t x) mutable {
+      enqueue_broadcast(a, w, root, *dsp, x, to);
+      if (!w.is_same(t) && rank_ != root) t.copy_(w);
+    });
   }, icp);
+  note_zc(zx);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(Coll::BROADCAST, a == Algo::IPC ? (ll ? "ipc_ll" : one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
   return work;
@@ -1725,12 +1747,16 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
   const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
   const char* algo = a == Algo::IPC ? (ll ? "ipc_ll" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
+  const bool zx = zc_exchanges(ds, a, cname, bytes);
   auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
-    enqueue_allgather(a, wi, wo, root, rooted, ds, s, to);
-    if (receiver)
-      for (int r = 0; r < size_; ++r)
-        if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
+      enqueue_allgather(a, wi, wo, root, rooted, *dsp, x, to);
+      if (receiver)
+        for (int r = 0; r < size_; ++r)
+          if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+    });
   }, icp);
+  note_zc(zx);
   record(cname, algo, bytes, t0);
   return work;
 }
@@ -1775,10 +1801,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
     ipc(ds);
     icp = ds.ipc;
   }
+  const bool zx = zc_exchanges(ds, a, Coll::SCATTER, bytes);
   auto work = gpu_run(Coll::SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    enqueue_scatter(a, wi, wo, root, ds, s, to);
-    if (!wo.is_same(out)) out.copy_(wo);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, out = out](hipStream_t x) mutable {
+      enqueue_scatter(a, wi, wo, root, *dsp, x, to);
+      if (!wo.is_same(out)) out.copy_(wo);
+    });
   }, icp);
+  note_zc(zx);
   record(Coll::SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl", bytes, t0);
   return work;
 }
@@ -1831,10 +1861,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     ipc(ds);
     icp = ds.ipc;
   }
+  const bool zx = zc_exchanges(ds, a, Coll::REDUCE_SCATTER, bytes);
   auto work = gpu_run(Coll::REDUCE_SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, ds, s, to);
-    if (!wo.is_same(out)) out.copy_(wo);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, out = out](hipStream_t x) mutable {
+      enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, *dsp, x, to);
+      if (!wo.is_same(out)) out.copy_(wo);
+    });
   }, icp);
+  note_zc(zx);
   record(Coll::REDUCE_SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
          bytes, t0);
   return work;
@@ -1886,11 +1920,15 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     ipc(ds);
     icp = ds.ipc;
   }
+  const bool zx = equal && zc_exchanges(ds, a, Coll::ALLTOALL, chunk);
   auto work = gpu_run(Coll::ALLTOALL, ds, keep, outs, to, [&](hipStream_t s) {
-    enqueue_alltoall(a, wi, wo, equal, ds, s, to);
-    for (size_t i = 0; i < outs.size(); ++i)
-      if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
+    ipc_issue(ds, a, s, zx, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
+      enqueue_alltoall(a, wi, wo, equal, *dsp, x, to);
+      for (size_t i = 0; i < outs.size(); ++i)
+        if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
+    });
   }, icp);
+  note_zc(zx);
   record(Coll::ALLTOALL, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(chunk) ? "ipc_ll" : "ipc") : "rccl", total,
          t0);
   return work;

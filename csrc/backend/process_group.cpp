@@ -103,25 +103,38 @@ c10::intrusive_ptr<c10::ivalue::Future> WorkMI355X::getFuture() {
 }
 
 // =================================================================== StreamSync
+// Words are allocated kSlabWords at a time, the first batch when the device state is
+// created: handing one out later makes no allocation and no memset -- both can
+// synchronise with streams that wait on the IPC launcher's thread.
+bool StreamSync::grow() {
+  // (signal memory comes in 8-byte allocations)
+  for (size_t i = 0; i < kSlabWords; ++i) {
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess || !p) {
+      (void)hipGetLastError();
+      return !spare.empty();
+    }
+    // signal memory is host-accessible: zero it from the host (no stream involved)
+    *static_cast<volatile uint64_t*>(p) = 0;
+    words.push_back(static_cast<uint64_t*>(p));
+    spare.push_back(static_cast<uint64_t*>(p));
+  }
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  return true;
+}
 uint64_t* StreamSync::alloc() {
+  std::lock_guard<std::mutex> lk(slab_mu);
   if (!ok) return nullptr;
-  void* p = nullptr;
-  if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess || !p) {
-    (void)hipGetLastError();
+  if (spare.empty() && !grow()) {
     ok = false;
     return nullptr;
   }
-  if (hipMemset(p, 0, sizeof(uint64_t)) != hipSuccess) {
-    (void)hipGetLastError();
-    (void)hipFree(p);
-    ok = false;
-    return nullptr;
-  }
-  return static_cast<uint64_t*>(p);
+  uint64_t* w = spare.back();
+  spare.pop_back();
+  return w;
 }
 StreamSync::~StreamSync() {
-  for (auto& kv : comm_done) (void)hipFree(kv.second.ptr);
-  for (auto& kv : user_ready) (void)hipFree(kv.second.ptr);
+  for (uint64_t* p : words) (void)hipFree(p);
 }
 
 // =================================================================== EventPool
@@ -394,6 +407,7 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
 }
 
 ProcessGroupMI355X::~ProcessGroupMI355X() {
+  stop_launchers();
   wd_stop_.store(true);
   if (wd_thr_.joinable()) wd_thr_.join();
   {
@@ -600,7 +614,11 @@ std::string ProcessGroupMI355X::describe() {
       << ", rccl_users=" << (kv.second->rccl ? kv.second->rccl->order().users() : 0)
       << ", rccl_issue_waits=" << (kv.second->rccl ? kv.second->rccl->order().waits() : 0)
       << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
-      << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0) << "}";
+      << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
+      << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
+      << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
+      << ", launcher_direct=" << (kv.second->launcher ? kv.second->launcher->direct : 0)
+      << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0) << "}";
   o << ")";
   return o.str();
 }
@@ -618,6 +636,7 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
         if (p.second->comm) p.second->comm->abort();
       }
       if (ds.ipc) ds.ipc->abort();  // kernels spinning in a cross-GPU barrier leave it
+      if (ds.launcher && ds.launcher->shm) ds.launcher->shm->abort();  // a job stuck in an exchange
     }
     if (shm_) shm_->abort();
   }
@@ -1171,19 +1190,27 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::recv(std::vector<at::Tensor>&
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::barrier(const c10d::BarrierOptions& opts) {
   before_op(Coll::BARRIER, {}, -1);
   const auto t0 = std::chrono::steady_clock::now();
+  std::vector<DeviceState*> dss;
   {
     std::lock_guard<std::mutex> lk(init_mu_);
-    for (auto& kv : devs_) {
-      PDCC_HIP(hipStreamSynchronize(kv.second->stream.stream()));
-      // synchronous collectives were enqueued on the caller's stream
-      PDCC_HIP(hipStreamSynchronize(
-            c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)kv.first).stream()));
-    }
+    for (auto& kv : devs_) dss.push_back(kv.second.get());
+  }
+  for (DeviceState* ds : dss) {
+    const hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds->device).stream();
+    launcher_quiesce(*ds, cur);  // every launcher job launched (host), cur ordered behind them
+    if (ds->launcher) PDCC_HIP(hipStreamSynchronize(ds->launcher->zs->stream()));
+    PDCC_HIP(hipStreamSynchronize(ds->stream.stream()));
+    // synchronous collectives were enqueued on the caller's stream
+    PDCC_HIP(hipStreamSynchronize(cur));
   }
   if (size_ > 1) {
     if (same_host_) shm().barrier(eff_timeout(opts.timeout));
     else store_barrier(store_, "pdcc/barrier/" + std::to_string(op_seq_.load()), rank_, size_);
   }
+  // every rank's IPC kernels have finished: release what the launcher's thread only queued
+  // (evicted mappings, outgrown staging)
+  for (DeviceState* ds : dss)
+    if (ds->ipc && ds->launcher) ds->ipc->maintain();
   record(Coll::BARRIER, same_host_ ? "shm" : "store", 0, t0);
   return cpu_done(Coll::BARRIER, {});
 }

@@ -27,6 +27,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <optional>
 #include <string>
 #include <thread>
 #include <tuple>
@@ -86,8 +87,19 @@ struct StreamSync {
   // per caller stream: the group comm stream's tick it has already waited for (a synchronous
   // collective on the caller's stream runs after every async collective issued before it)
   std::map<hipStream_t, uint64_t> comm_seen;
-  uint64_t* alloc();                             // nullptr when unavailable
+  uint64_t* alloc();                             // nullptr when unavailable (thread-safe)
+  bool prealloc() {                              // the first slab, at device-state creation
+    std::lock_guard<std::mutex> lk(slab_mu);
+    return !words.empty() || grow();
+  }
   ~StreamSync();
+
+ private:
+  static constexpr size_t kSlabWords = 32;
+  bool grow();
+  std::mutex slab_mu;
+  std::vector<uint64_t*> words;  // every word allocated (freed with the state)
+  std::vector<uint64_t*> spare;  // not handed out yet
 };
 
 // Completion gate of a GPU work whose enqueue is deferred to another thread (the
@@ -187,6 +199,47 @@ struct PairChan {
   explicit PairChan(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
 };
 
+// Deferred IPC launches (PDCC_IPC_ZC_ASYNC). A zero-copy IPC call needs every rank's
+// buffer record (allocation handle + offset) before its kernel can be launched, i.e. a
+// host-side exchange with the peers. Done on the caller's thread, that exchange would
+// line up the hosts of all ranks at every such call -- an async bucket all-reduce fired
+// from a backward hook would stall that rank's backward until every peer reached the
+// same bucket. Instead the call becomes a job of this per-device launcher thread:
+//   caller: stream s writes its `ready` tick, s waits `done` >= ticket, return;
+//   helper: exchange (own host channel), open mappings, then on its launch stream zs:
+//           wait `ready` tick, launch the kernels, write `done` = ticket.
+// Any IPC launch of the group issued while jobs are pending becomes a job too (FIFO), so
+// the device sees the group's IPC kernels in issue order on every rank; with the
+// launcher idle, non-exchanging launches (LL, staged) go straight to s. Graph capture
+// and autotune races drain the launcher first and run inline.
+struct IpcLauncher {
+  struct Job {
+    std::function<void(hipStream_t)> fn;
+    uint64_t* ready;
+    uint64_t ready_tick;
+    uint64_t ticket;
+  };
+  std::mutex mu;
+  std::condition_variable cv;       // jobs / stop
+  std::condition_variable idle_cv;  // queue drained and no job running
+  std::deque<Job> q;
+  bool busy = false, stop = false;
+  std::thread thr;
+  std::optional<c10::hip::HIPStreamMasqueradingAsCUDA> zs;  // the jobs' launch stream
+  uint64_t* done = nullptr;          // signal memory: ticket of the last launched job (on zs)
+  uint64_t next_ticket = 0;          // tickets handed out so far
+  std::map<hipStream_t, SignalWord> ready;   // per submitting stream
+  std::map<hipStream_t, uint64_t> seen;      // per stream: tickets it already waits for
+  std::unique_ptr<host::ShmComm> shm;        // the helper's own host channel (exchanges)
+  std::string error;
+  uint64_t jobs = 0, direct = 0, fallbacks = 0;
+};
+
+// launcher.cpp: the exchange channel of a launcher job's thread (nullptr elsewhere), and
+// whether `s` is being captured into a graph
+extern thread_local host::ShmComm* tls_xchg;
+bool capturing_stream(hipStream_t s);
+
 struct DeviceState {
   int device = -1;
   c10::hip::HIPStreamMasqueradingAsCUDA stream;  // comm stream for async collectives (PDCC_STREAM)
@@ -206,6 +259,7 @@ struct DeviceState {
   std::map<int, bool> pair_distinct;               // peer on another device (RCCL-capable pair)?
   std::shared_ptr<EventPool> events = std::make_shared<EventPool>();
   std::shared_ptr<StreamSync> sync = std::make_shared<StreamSync>();
+  std::unique_ptr<IpcLauncher> launcher;  // lazy (PDCC_IPC_ZC_ASYNC)
   explicit DeviceState(c10::hip::HIPStreamMasqueradingAsCUDA s) : stream(s) {}
 };
 
@@ -368,6 +422,18 @@ class ProcessGroupMI355X : public c10d::Backend {
   // the staged rest is the same call with every in/out pointer moved past the body.
   void ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                size_t per_call_max, hipStream_t s, const char* selftest = nullptr);
+  // Issue the enqueue `fn` of engine `a` on stream `s`: RCCL/host engines and IPC with the
+  // launcher idle run now; an IPC call that exchanges zero-copy records (`exchanges`), or any
+  // IPC call while jobs are pending, becomes a launcher job (IpcLauncher). launcher.cpp
+  void ipc_issue(DeviceState& ds, Algo a, hipStream_t s, bool exchanges, std::function<void(hipStream_t)> fn);
+  // will this IPC call run a zero-copy exchange (group-wide facts only)
+  bool zc_exchanges(DeviceState& ds, Algo a, Coll c, size_t bytes) const;
+  void note_zc(bool exchanges);
+  IpcLauncher& launcher(DeviceState& ds);
+  void launcher_loop(DeviceState* ds, IpcLauncher* l);
+  // host-wait until the launcher has launched every job, and order `s` behind them
+  void launcher_quiesce(DeviceState& ds, hipStream_t s);
+  void stop_launchers();
 
   // p2p on CPU runs on two background threads (so isend/irecv pairs never deadlock)
   struct Job {

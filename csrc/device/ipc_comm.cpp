@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <utility>
 
@@ -48,10 +49,13 @@ std::pair<void*, void*> open_handle(const std::vector<uint8_t>& b) {
 // and then refuses to export it (hipIpcGetMemHandle: invalid argument). Such a
 // block is held (so the next try gets a different range) and freed once an
 // exportable one is found. `uncached` selects fine-grained memory (signals).
-void* alloc_exportable(size_t bytes, bool uncached, std::vector<uint8_t>& blob) {
+void* alloc_exportable(size_t bytes, bool uncached, std::vector<uint8_t>& blob, std::vector<void*>* defer = nullptr) {
   std::vector<void*> refused;
-  auto release = [&] {
-    for (void* q : refused) hipFree(q);
+  auto release = [&] {  // (deferred: hipFree synchronises the device, see IpcComm::defer_frees)
+    for (void* q : refused) {
+      if (defer) defer->push_back(q);
+      else hipFree(q);
+    }
   };
   for (int attempt = 0; attempt < 6; ++attempt) {
     void* p = nullptr;
@@ -110,6 +114,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       timeout_ticks_(timeout_ms * 100000ull),  // s_memrealtime runs at 100 MHz
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
+  if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
@@ -133,7 +138,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
         PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&trace_dev_), trace_host_, 0));
       }
     }
-    PDCC_HIP(hipDeviceSynchronize());
+    PDCC_HIP(hipStreamSynchronize(nullptr));  // the memset (null stream) is done before peers map it
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();  // published empty: the peers fail this step with us
@@ -165,9 +170,14 @@ IpcComm::~IpcComm() {
       if (r.mine) hipFree(r.mine);
     }
     retired_.clear();
+    for (void* q : deferred_free_) hipFree(q);
+    deferred_free_.clear();
+    reap_closing(true);
     for (auto& peer : zc_imports_)
-      for (auto& im : peer)
+      for (auto& im : peer) {
+        if (im.last && im.last->ev) (void)hipEventSynchronize(im.last->ev);
         if (im.map) hipIpcCloseMemHandle(im.map);
+      }
     zc_imports_.clear();
     for (void* m : flags_maps_)
       if (m) hipIpcCloseMemHandle(m);
@@ -178,9 +188,13 @@ IpcComm::~IpcComm() {
   }
 }
 
+thread_local bool IpcComm::tls_defer_frees_ = false;
+
 void IpcComm::unmap_staging() {
-  if (graph_mode_) {
-    // a captured graph has these buffers baked into its kernel arguments: keep them alive
+  if (graph_mode_ || tls_defer_frees_) {
+    // a captured graph has these buffers baked into its kernel arguments, or this is the
+    // IPC launcher's thread (hipFree / hipIpcCloseMemHandle synchronise the device, and
+    // streams wait on this thread): keep them alive until maintain() / the group's end
     if (my_staging_) retired_.push_back({my_staging_, staging_maps_});
   } else {
     for (void* m : staging_maps_)
@@ -200,7 +214,7 @@ void IpcComm::map_staging(size_t cap) {
   std::string err;
   char* fresh = nullptr;
   try {
-    fresh = static_cast<char*>(alloc_exportable(granule(cap), false, mine));
+    fresh = static_cast<char*>(alloc_exportable(granule(cap), false, mine, tls_defer_frees_ ? &deferred_free_ : nullptr));
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();
@@ -237,6 +251,7 @@ void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
   DeviceScope ds(device_);
   size_t cap = std::max<size_t>(bytes, 4u << 20);
   cap = std::max(cap, std::min(max_staging_, cap_ * 2));
+  if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: staging %zu -> %zu B\n", rank_, cap_, cap);
   // nobody may still read the old buffers: drain locally, then agree globally
   PDCC_HIP(hipStreamSynchronize(stream));
   ++staging_gen_;
@@ -339,6 +354,7 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
       for (auto v = zc_exports_.begin(); v != zc_exports_.end(); ++v)
         if (!v->pinned && (victim == zc_exports_.end() || v->last < victim->last)) victim = v;
       if (victim != zc_exports_.end()) {
+        if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: evict export id %llu\n", rank_, (unsigned long long)victim->id);
         r.evict = victim->id;
         zc_exports_.erase(victim);
       }
@@ -361,24 +377,53 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   return r;
 }
 
+IpcComm::LaunchEvent::~LaunchEvent() {
+  if (ev) (void)hipEventDestroy(ev);
+}
+
+void IpcComm::reap_closing(bool wait_all) {
+  std::lock_guard<std::mutex> lk(closing_mu_);
+  size_t keep = 0;
+  for (size_t i = 0; i < zc_closing_.size(); ++i) {
+    Closing& c = zc_closing_[i];
+    bool done = !c.last || !c.last->ev;
+    if (!done) {
+      const hipError_t e = wait_all ? hipEventSynchronize(c.last->ev) : hipEventQuery(c.last->ev);
+      done = e != hipErrorNotReady;
+      (void)hipGetLastError();
+    }
+    if (done) {
+      if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
+      if (c.map) hipIpcCloseMemHandle(c.map);
+    } else {
+      zc_closing_[keep++] = std::move(c);
+    }
+  }
+  zc_closing_.resize(keep);
+}
+
 bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
   DeviceScope ds(device_);
-  // evictions first, whatever the outcome of this exchange (keeps the caches in step)
-  bool drained = false;
+  if (!tls_defer_frees_) reap_closing(false);
+  // evictions first, whatever the outcome of this exchange (keeps the caches in step); an
+  // in-flight kernel of this rank may still read through the mapping: the close waits for
+  // the last launch that used it (reap_closing), not for the whole device
   for (int r = 0; r < world_; ++r) {
     if (r == rank_ || all[r].evict == 0) continue;
     auto& peer = zc_imports_[r];
     auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].evict; });
     if (it == peer.end()) continue;
-    if (!drained) {  // an in-flight kernel of this rank may still read through the mapping
-      PDCC_HIP(hipDeviceSynchronize());
-      drained = true;
+    {
+      std::lock_guard<std::mutex> lk(closing_mu_);
+      zc_closing_.push_back({it->map, it->last});
     }
-    hipIpcCloseMemHandle(it->map);
     peer.erase(it);
   }
+  if (!tls_defer_frees_) reap_closing(false);
+  zc_cur_ids_.assign(world_, 0);
   if (!all_ok) return false;
   ptrs.assign(world_, nullptr);
+  if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: import (%zu closing)\n", rank_, zc_closing_.size());
   bool ok = true;
   for (int r = 0; r < world_; ++r) {
     if (r == rank_) {
@@ -390,6 +435,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
     auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].id; });
     if (it == peer.end()) {
       void* m = nullptr;
+      if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: open id %llu of rank %d\n", rank_, (unsigned long long)all[r].id, r);
       if (hipIpcOpenMemHandle(&m, all[r].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !m) {
         (void)hipGetLastError();
         if (!all[r].fresh)  // every rank mapped it when it was fresh: this cannot be agreed on any more
@@ -398,9 +444,10 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
         ok = false;
         continue;
       }
-      peer.push_back({all[r].id, m});
+      peer.push_back({all[r].id, m, nullptr});
       it = peer.end() - 1;
     }
+    zc_cur_ids_[r] = all[r].id;
     ptrs[r] = static_cast<char*>(it->map) + all[r].off;
   }
   return ok;
@@ -421,7 +468,40 @@ void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipS
   if ((int)bufs.size() != world_) throw std::runtime_error("pdcc: zero-copy IPC launch without every rank's buffer");
   call.zc = 1;
   prepare_staging(call, stream);  // (a rooted reduce stages its reduced tiles)
+  if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: launch zc %zu B\n", rank_, call.bytes);
   launch_view(view(bufs), call, stream);
+  // the mappings this launch reads through stay open until it has finished (eviction);
+  // a captured launch reads exports pinned for the graph's lifetime (never evicted)
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  auto le = std::make_shared<LaunchEvent>();
+  DeviceScope ds(device_);
+  PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
+  PDCC_HIP(hipEventRecord(le->ev, stream));
+  for (int r = 0; r < world_ && r < (int)zc_cur_ids_.size(); ++r) {
+    if (r == rank_ || zc_cur_ids_[r] == 0) continue;
+    for (auto& im : zc_imports_[r])
+      if (im.id == zc_cur_ids_[r]) im.last = le;
+  }
+}
+
+void IpcComm::maintain() {
+  DeviceScope ds(device_);
+  reap_closing(true);
+  if (graph_mode_) return;
+  for (auto& r : retired_) {
+    for (void* m : r.maps)
+      if (m) hipIpcCloseMemHandle(m);
+    if (r.mine) hipFree(r.mine);
+  }
+  retired_.clear();
+  for (void* q : deferred_free_) hipFree(q);
+  deferred_free_.clear();
+}
+
+size_t IpcComm::zc_closing() const {
+  std::lock_guard<std::mutex> lk(closing_mu_);
+  return zc_closing_.size();
 }
 
 size_t IpcComm::zc_mappings() const {

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime_api.h>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -100,6 +102,20 @@ class IpcComm {
   void launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream);
   size_t zc_exports() const { return zc_exports_.size(); }
   size_t zc_mappings() const;
+  // evicted mappings not closed yet (their last launch may still run, or no safe point came)
+  size_t zc_closing() const;
+
+  // The IPC launcher's thread (ProcessGroupMI355X) sets this: hipFree and hipIpcCloseMemHandle
+  // synchronise the whole device, and the callers' streams wait on that thread's launches --
+  // there, evicted mappings and outgrown staging are only queued, never released.
+  static void set_thread_defers_frees(bool v) { tls_defer_frees_ = v; }
+  // Release what was queued: close evicted mappings whose last launch finished (waits for
+  // it), free retired staging. Call only with no IPC work of this communicator in flight
+  // and no stream waiting on the launcher (barrier, shutdown).
+  void maintain();
+  // close the evicted mappings whose last launch has finished (wait_all: wait for all);
+  // synchronises the device like any hipIpcCloseMemHandle -- not on the launcher's thread
+  void reap_closing(bool wait_all);
 
  private:
   void map_staging(size_t cap);
@@ -117,10 +133,28 @@ class IpcComm {
     bool pinned;
     uint64_t last;  // LRU tick
   };
+  // completion of one zero-copy launch (recorded on its stream right after it)
+  struct LaunchEvent {
+    hipEvent_t ev = nullptr;
+    ~LaunchEvent();
+  };
   struct ZcImport {
     uint64_t id;
     void* map;  // hipIpcOpenMemHandle result (allocation base on this side)
+    std::shared_ptr<LaunchEvent> last;  // the latest launch that read through this mapping
   };
+  // Evicted mappings are closed once the last launch that used them has finished (polled
+  // at every exchange; the destructor waits): no device-wide synchronisation, so compute
+  // streams and point-to-point pair streams are never drained by an eviction.
+  struct Closing {
+    void* map;
+    std::shared_ptr<LaunchEvent> last;
+  };
+  mutable std::mutex closing_mu_;
+  std::vector<Closing> zc_closing_;
+  static thread_local bool tls_defer_frees_;
+  std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread
+  std::vector<uint64_t> zc_cur_ids_;  // per peer: the allocation id mapped by the last zc_import
   std::vector<ZcExport> zc_exports_;
   std::vector<std::vector<ZcImport>> zc_imports_;  // per peer
   size_t zc_cache_ = 16;
@@ -131,6 +165,7 @@ class IpcComm {
   c10::intrusive_ptr<c10d::Store> store_;
   std::string key_;
   int rank_, world_, device_;
+  int log_ = 0;  // PDCC_LOG_LEVEL >= 3: staging growth, mapping opens / closes
   size_t max_staging_;
   uint64_t timeout_ticks_;
   bool shared_device_;

@@ -23,8 +23,9 @@ bool IssueOrder::ensure_word() {
   if (word_ || (dry_ && !word_failed_)) return true;
   if (word_failed_) return false;
   void* p = nullptr;
-  if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess && p &&
-      hipMemset(p, 0, sizeof(uint64_t)) == hipSuccess) {
+  if (hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) == hipSuccess && p) {
+    *static_cast<volatile uint64_t*>(p) = 0;  // host-accessible: no null-stream memset
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
     word_ = static_cast<uint64_t*>(p);
     return true;
   }

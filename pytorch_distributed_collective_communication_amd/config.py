@@ -16,6 +16,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_COPY_MAX | 1M | gather/scatter/all-gather/reduce-scatter/all-to-all up to this: IPC |
 | PDCC_IPC_MAX_STAGING | 1G | staging bytes; larger calls are chunked |
 | PDCC_IPC_SPIN_MS | 600000 | bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if shorter) |
+| PDCC_IPC_ZC_ASYNC | 1 | zero-copy calls exchange their buffer records on a per-device launcher thread: the caller's host never waits for its peers (0: inline exchange) |
 | PDCC_IPC_LL_MAX | 64K | all-reduces up to this size (max 64K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
@@ -81,6 +82,7 @@ class Config:
     ipc_zc_min: int = 1 << 20
     ipc_ll_max: int = 64 << 10
     ipc_zc_cache: int = 16
+    ipc_zc_async: bool = True
     ipc_spin_ms: int = 600000
     ipc_grid: int = 512
     ipc_wide_grid: int = 1024
@@ -118,7 +120,7 @@ _ENV = {
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
-    "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "autotune": "PDCC_AUTOTUNE",
+    "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",

@@ -51,6 +51,13 @@ for s in "$@"; do
         -d "$0/gpurun_out/prof_stg" -o stg -- python3 "$0/scripts/zc_bench.py" --sizes 64M --iters 8 --modes staged' "$(pwd)" ;;
     conf) step conf 900 python -u -m pytest tests/test_backend_gpu.py -x -v --timeout 300 --timeout-method thread \
         -k "conformance or list_all_to_all or ll_reduce_scatter or world8 or async or autotune" ;;
+    zcasync) step zcasync 600 python -u -m pytest tests/test_backend_gpu.py -x -v --timeout 300 --timeout-method thread \
+        -k "zero_copy or zc or churn or conformance or push or async" ;;
+    zerobench) step zerobench 600 python scripts/zero_bench.py ;;
+    zcdebug) step zcdebug 150 python scripts/zc_debug.py zero_copy --world 3 --dump-s 60 \
+        --env PDCC_ALGO=ipc PDCC_IPC_ZC_CACHE=4 PDCC_IPC_1SHOT_MAX=256K ;;
+    atsdebug) step atsdebug 150 python scripts/zc_debug.py async_then_sync --world 2 --dump-s 40 \
+        --env PDCC_ALGO=ipc ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;

@@ -1343,3 +1343,71 @@ def conformance_probe(rank, size, device="cuda", max_bytes=64 << 20):
     from pytorch_distributed_collective_communication_amd.utils import conformance
 
     return conformance.run(rank, size, _dev(device), deadline_s=120.0, max_bytes=max_bytes)
+
+
+def zc_async_probe(rank, size, device="cuda", trials=5, n=16 << 20, late_ms=50):
+    """Zero-copy calls exchange their buffer records on the launcher thread: rank 0's
+    host must get an async 64 MiB all_reduce back at once while rank 1 is held back
+    `late_ms`; a synchronous one as well (only the stream waits). Values checked."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    x = torch.full((n,), float(rank + 1), device=d)
+    dist.all_reduce(x)  # first call: fresh export, mappings made and confirmed
+    torch.cuda.synchronize()
+    tri = size * (size + 1) / 2
+    res = {"warm": bool(torch.all(x == tri)), "algo": b.last_algo()}
+    for mode in ("async", "sync"):
+        ret, ok = [], True
+        for _ in range(trials):
+            x.fill_(float(rank + 1))
+            torch.cuda.synchronize()
+            dist.barrier()
+            if rank == 1:
+                time.sleep(late_ms / 1e3)
+            t0 = time.perf_counter()
+            w = dist.all_reduce(x, async_op=(mode == "async"))
+            ret.append((time.perf_counter() - t0) * 1e6)
+            if w is not None:
+                w.wait()
+            torch.cuda.synchronize()
+            ok = ok and bool(torch.all(x == tri))
+        res[f"{mode}_ret_us"] = statistics.median(ret)
+        res[f"{mode}_ok"] = ok
+    res["desc"] = b.describe()
+    return res
+
+
+def zc_churn_probe(rank, size, device="cuda", allocs=40, n=(1 << 20) // 4 + 64):
+    """More distinct >= 1 MiB allocations than the zero-copy cache holds: exports get
+    evicted and their mappings closed once the last launch that read them is done (no
+    device-wide sync); every result right, the closing list drains."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    bufs = [torch.full((n + 64 * i,), float(rank + i), device=d) for i in range(allocs)]
+    ok = True
+    for rnd in range(2):
+        for i, t in enumerate(bufs):
+            t.fill_(float(rank + i))
+            w = dist.all_reduce(t, async_op=True)
+            if i % 3 == 0:
+                w.wait()
+        torch.cuda.synchronize()
+        for i, t in enumerate(bufs):
+            ok = ok and bool(torch.all(t == sum(r + i for r in range(size))))
+    dist.barrier()
+    x = torch.ones(n, device=d)
+    dist.all_reduce(x)  # one more exchange: reaps what finished
+    torch.cuda.synchronize()
+    return {"ok": ok, "algo": b.last_algo(), "desc": b.describe()}

@@ -127,7 +127,7 @@ def test_python_config_mirror_matches_the_backend(env):
     cpp = dict(re.findall(r"(\w+)=(\S+)", desc))
     for key in ("ipc_1shot_max", "ipc_2shot_max", "ipc_copy_max", "ipc_max_staging", "ipc_zc", "ipc_zc_min",
                 "ipc_zc_cache", "ipc_push", "ipc_spin_ms", "ipc_grid", "ipc_wide_grid", "ipc_ll_max", "autotune", "autotune_sample", "algo",
-                "rccl_wide_ctas", "rccl_wide_min", "a2a_list_agree"):
+                "rccl_wide_ctas", "rccl_wide_min", "a2a_list_agree", "ipc_zc_async"):
         want = py[key]
         got = cpp[key].rstrip(",)")
         assert got == (str(int(want)) if isinstance(want, bool) else str(want)), (key, got, want)
