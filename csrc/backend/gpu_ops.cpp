@@ -860,7 +860,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
   } else {  // (a launcher job exchanges on the launcher's own channel)
     std::vector<void*> outs;
     for (auto& r : all) outs.push_back(&r);
-    (tls_xchg ? *tls_xchg : shm()).allgather(&mine, outs, sizeof(mine), timeout_);
+    (cfg_.ipc_zc_async ? exchange_channel(ds) : shm()).allgather(&mine, outs, sizeof(mine), timeout_);
   }
   bool all_ok = true, fresh = false;
   for (const auto& r : all) {
@@ -876,7 +876,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
       for (const auto& x : v) ok = ok && !x.empty() && x[0] == 1;
     } else {
       double f = ok ? 1.0 : 0.0;
-      (tls_xchg ? *tls_xchg : shm()).allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
+      (cfg_.ipc_zc_async ? exchange_channel(ds) : shm()).allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
       ok = f > 0.0;
     }
   }
@@ -886,7 +886,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
   if (call.coll == kern::IpcColl::REDUCE_2SHOT || call.coll == kern::IpcColl::ALLREDUCE_PUSH) {
     // the rooted reduce stages its reduced tiles, the push all-reduce receives its owned
     // tiles in staging: chunks of at most the staging cap
-    const size_t chunk = std::max(unit, ic.max_staging() / unit * unit);
+    const size_t chunk = std::max(unit, ic.chunk_cap() / unit * unit);
     for (size_t off = 0; off < body; off += chunk) {
       kern::IpcCall c = call;
       c.bytes = std::min(chunk, body - off);
@@ -904,13 +904,19 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
 
 void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                                  size_t per_call_max, hipStream_t s, const char* selftest) {
-  const size_t body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
-  if (!tls_xchg) {  // (a launcher job: the caller already recorded the call as zero-copy)
+  size_t body = 0;
+  if (!selftest && cfg_.ipc_zc_async && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
+      !capturing(s)) {
+    // gated launches now, the exchange on the exchange thread (launcher.cpp)
+    body = call.bytes / unit * unit;
+    if (body) ipc_gated(ds, call, zbuf, zlen, unit, body, per_call_max, s);
+  } else {
+    if (!selftest) launcher_quiesce(ds);  // inline exchange: the channel is this thread's now
+    body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
+  }
+  {
     std::lock_guard<std::mutex> lk(stats_mu_);
     zc_ran_ = body > 0;
-  } else if (body == 0 && ds.launcher) {
-    std::lock_guard<std::mutex> lk(ds.launcher->mu);
-    ++ds.launcher->fallbacks;  // recorded as zero-copy, ran staged (a rank could not export)
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;
@@ -934,7 +940,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
                                                            std::chrono::milliseconds timeout,
                                                            const std::function<void(hipStream_t)>& fn,
                                                            std::shared_ptr<IpcComm> ipcp,
-                                                           const c10::hip::HIPStreamMasqueradingAsCUDA* stream) {
+                                                           const c10::hip::HIPStreamMasqueradingAsCUDA* stream,
+                                                           bool self_timed) {
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
   auto cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds.device);
   // synchronous collectives (and PDCC_STREAM=current) run on the caller's stream: no
@@ -997,32 +1004,23 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   }
   hipEvent_t ev = nullptr;
   uint64_t done_tick = 0;
+  // A synchronous collective on the caller's stream whose kernels bound their own spins
+  // (IPC: a stuck peer sets the error word the watchdog polls) needs no completion marker:
+  // its Work is done as far as the caller's stream goes (no event record, ~1 us per call)
+  const bool marker = !(self_timed && comm == cur && !cfg_.blocking_wait);
   if (use_sig) {
     std::lock_guard<std::mutex> lk(sy.mu);
     done_tick = ++done_word->next;
     PDCC_HIP(hipStreamWriteValue64(comm.stream(), done_word->ptr, done_tick, 0));
-  } else {
+  } else if (marker) {
     ev = ds.events->get();
     PDCC_HIP(hipEventRecord(ev, comm.stream()));
   }
-  auto w = c10::make_intrusive<WorkMI355X>(rank_, [c] {
-    switch (c) {
-      case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
-      case Coll::REDUCE: return c10d::OpType::REDUCE;
-      case Coll::BROADCAST: return c10d::OpType::BROADCAST;
-      case Coll::ALLGATHER: return c10d::OpType::ALLGATHER;
-      case Coll::GATHER: return c10d::OpType::GATHER;
-      case Coll::SCATTER: return c10d::OpType::SCATTER;
-      case Coll::REDUCE_SCATTER: return c10d::OpType::REDUCE_SCATTER;
-      case Coll::ALLTOALL: return c10d::OpType::ALLTOALL;
-      case Coll::SEND: return c10d::OpType::SEND;
-      case Coll::RECV: return c10d::OpType::RECV;
-      default: return c10d::OpType::BARRIER;
-    }
-  }(), op_seq_.load(), std::move(outputs), c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, comm,
+  auto w = c10::make_intrusive<WorkMI355X>(rank_, op_type(c), op_seq_.load(), std::move(outputs),
+                                           c10::Device(c10::kCUDA, (c10::DeviceIndex)ds.device), ev, comm,
                                            health_, cfg_.blocking_wait, timeout, std::move(ipcp), ds.events);
   if (use_sig) w->set_signal(ds.sync, done_word->ptr, done_tick);
-  if (cfg_.watchdog_ms > 0) {
+  if (cfg_.watchdog_ms > 0 && (marker || use_sig)) {
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.emplace_back(w);
   }
@@ -1048,13 +1046,36 @@ void ProcessGroupMI355X::order_after_async(DeviceState& ds, hipStream_t s) {
   }
 }
 
-// A call handed to the IPC launcher runs its zero-copy exchange later, on the launcher's
-// thread: it is recorded as zero-copy now (a rank that cannot export makes it fall back to
-// staging; the launcher counts those, describe() "zc_fallbacks")
-void ProcessGroupMI355X::note_zc(bool exchanges) {
-  if (!exchanges || !cfg_.ipc_zc_async) return;
-  std::lock_guard<std::mutex> lk(stats_mu_);
-  zc_ran_ = true;
+c10d::OpType ProcessGroupMI355X::op_type(Coll c) {
+  switch (c) {
+    case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
+    case Coll::REDUCE: return c10d::OpType::REDUCE;
+    case Coll::BROADCAST: return c10d::OpType::BROADCAST;
+    case Coll::ALLGATHER: return c10d::OpType::ALLGATHER;
+    case Coll::GATHER: return c10d::OpType::GATHER;
+    case Coll::SCATTER: return c10d::OpType::SCATTER;
+    case Coll::REDUCE_SCATTER: return c10d::OpType::REDUCE_SCATTER;
+    case Coll::ALLTOALL: return c10d::OpType::ALLTOALL;
+    case Coll::SEND: return c10d::OpType::SEND;
+    case Coll::RECV: return c10d::OpType::RECV;
+    default: return c10d::OpType::BARRIER;
+  }
+}
+
+c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_issue(Coll c, DeviceState& ds, Algo a,
+                                                             const std::vector<at::Tensor>& keep_alive,
+                                                             std::vector<at::Tensor> outputs,
+                                                             std::chrono::milliseconds timeout,
+                                                             std::function<void(hipStream_t)> job,
+                                                             std::shared_ptr<IpcComm> ipcp) {
+  hp_.lap(HostStage::CHOOSE);
+  auto w = gpu_run(c, ds, keep_alive, std::move(outputs), timeout, [&](hipStream_t s) {
+    hp_.lap(HostStage::PRE);
+    job(s);
+    hp_.lap(HostStage::ENQUEUE);
+  }, std::move(ipcp), nullptr, /*self_timed=*/is_ipc(a));
+  hp_.lap(HostStage::WORK);
+  return w;
 }
 
 // =================================================================== autotuner
@@ -1114,10 +1135,9 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
     if (is_ipc(a)) ipc(ds);
   }
   // the race runs on the caller's stream: it must not overlap an async collective of this
-  // group still in flight on the comm stream or the IPC launcher's stream (IPC kernels of
-  // one rank share the per-block counters, the staging buffer and the LL epoch word)
+  // group still in flight on the comm stream (IPC kernels of one rank share the per-block
+  // counters, the staging buffer and the LL epoch word)
   order_after_async(ds, current_stream(ds.device));
-  launcher_quiesce(ds, current_stream(ds.device));
   return tune(key, cands);
 }
 
@@ -1302,9 +1322,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     // rooted reduce: into staging, so non-root tensors stay untouched)
     if (c.coll == kern::IpcColl::ALLREDUCE_2SHOT || c.coll == kern::IpcColl::REDUCE_2SHOT ||
         c.coll == kern::IpcColl::ALLREDUCE_PUSH)
-      ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
+      ipc_run(ds, c, w.data_ptr(), w.nbytes(), (size_t)size_ * kern::kTileBytes, ic.chunk_cap(), s);
     else
-      ipc_chunked(ic, c, ic.max_staging(), s);
+      ipc_chunked(ic, c, ic.chunk_cap(), s);
   } else if (is_rccl(a)) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
     RcclComm& rc = a == Algo::RCCL_WIDE ? rccl_wide(ds) : rccl(ds);
@@ -1339,9 +1359,9 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
       return;
     }
     if (c.coll == kern::IpcColl::BROADCAST_2SHOT)
-      ipc_run(ds, c, w.data_ptr(), bytes, (size_t)size_ * kern::kTileBytes, ic.max_staging(), s);
+      ipc_run(ds, c, w.data_ptr(), bytes, (size_t)size_ * kern::kTileBytes, ic.chunk_cap(), s);
     else
-      ipc_chunked(ic, c, ic.max_staging(), s);
+      ipc_chunked(ic, c, ic.chunk_cap(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
@@ -1375,7 +1395,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
       ic.launch(c, s);
       return;
     }
-    ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.max_staging(), s);
+    ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.chunk_cap(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
@@ -1441,7 +1461,7 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
     }
     // a flat root list (e.g. x.chunk(W)) is read in place; the other ranks share nothing
     const void* z = rank_ == root ? (is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr) : nullptr;
-    ipc_run(ds, c, z, rank_ == root ? bytes * size_ : 0, kern::kTileBytes, ic.max_staging() / size_, s);
+    ipc_run(ds, c, z, rank_ == root ? bytes * size_ : 0, kern::kTileBytes, ic.chunk_cap() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
@@ -1493,7 +1513,7 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
     }
     // a flat input (reduce_scatter_tensor) is read in place by every peer
     ipc_run(ds, c, is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr, bytes * size_, kern::kTileBytes,
-            ic.max_staging() / size_, s);
+            ic.chunk_cap() / size_, s);
   } else if (a == Algo::RCCL) {
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", wo.scalar_type());
     RcclComm& rc = rccl(ds);
@@ -1546,7 +1566,7 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
       return;
     }
     ipc_run(ds, c, is_flat(wi, c.bytes) ? wi[0].data_ptr() : nullptr, c.bytes * size_, kern::kTileBytes,
-            ic.max_staging() / size_, s);
+            ic.chunk_cap() / size_, s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
@@ -1598,6 +1618,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     return cpu_done(cname, {t});
   }
   DeviceState& ds = dev_state(t);
+  hp_.lap(HostStage::DEV_STATE);
   kern::DType kd;
   kern::RedOp ko;
   const bool kok = kern_dtype(t.scalar_type(), kd) && kern_op(op, ko) && kern::supports(kd, ko);
@@ -1630,14 +1651,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     icp = ds.ipc;
   }
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
-  const bool zx = zc_exchanges(ds, a, cname, bytes);
-  auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, t = t](hipStream_t x) mutable {
-      enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, *dsp, x, to);
-      if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
-    });
+  auto work = gpu_issue(cname, ds, a, {t, w}, {t}, to, [=, dsp = &ds, t = t](hipStream_t x) mutable {
+    enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, *dsp, x, to);
+    if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
   }, icp);
-  note_zc(zx);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
                              : one_shot                         ? "ipc_1shot"
@@ -1645,6 +1662,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
                              : a == Algo::IPC_WIDE            ? "ipc_2shot_wide"
                                                               : "ipc_2shot")
                           : a == Algo::RCCL_WIDE ? "rccl_wide" : "rccl", bytes, t0);
+  hp_.lap(HostStage::RECORD);
   return work;
 }
 
@@ -1682,14 +1700,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     icp = ds.ipc;
   }
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
-  const bool zx = zc_exchanges(ds, a, Coll::BROADCAST, bytes);
-  auto work = gpu_run(Coll::BROADCAST, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, t = t](hipStream_t x) mutable {
-      enqueue_broadcast(a, w, root, *dsp, x, to);
-      if (!w.is_same(t) && rank_ != root) t.copy_(w);
-    });
+  auto work = gpu_issue(Coll::BROADCAST, ds, a, {t, w}, {t}, to, [=, dsp = &ds, t = t](hipStream_t x) mutable {
+    enqueue_broadcast(a, w, root, *dsp, x, to);
+    if (!w.is_same(t) && rank_ != root) t.copy_(w);
   }, icp);
-  note_zc(zx);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(Coll::BROADCAST, a == Algo::IPC ? (ll ? "ipc_ll" : one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
   return work;
@@ -1747,16 +1761,12 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
   const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
   const char* algo = a == Algo::IPC ? (ll ? "ipc_ll" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
-  const bool zx = zc_exchanges(ds, a, cname, bytes);
-  auto work = gpu_run(cname, ds, keep, outs, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
-      enqueue_allgather(a, wi, wo, root, rooted, *dsp, x, to);
-      if (receiver)
-        for (int r = 0; r < size_; ++r)
-          if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
-    });
+  auto work = gpu_issue(cname, ds, a, keep, outs, to, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
+    enqueue_allgather(a, wi, wo, root, rooted, *dsp, x, to);
+    if (receiver)
+      for (int r = 0; r < size_; ++r)
+        if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
   }, icp);
-  note_zc(zx);
   record(cname, algo, bytes, t0);
   return work;
 }
@@ -1801,14 +1811,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
     ipc(ds);
     icp = ds.ipc;
   }
-  const bool zx = zc_exchanges(ds, a, Coll::SCATTER, bytes);
-  auto work = gpu_run(Coll::SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, out = out](hipStream_t x) mutable {
-      enqueue_scatter(a, wi, wo, root, *dsp, x, to);
-      if (!wo.is_same(out)) out.copy_(wo);
-    });
+  auto work = gpu_issue(Coll::SCATTER, ds, a, keep, {out}, to, [=, dsp = &ds, out = out](hipStream_t x) mutable {
+    enqueue_scatter(a, wi, wo, root, *dsp, x, to);
+    if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  note_zc(zx);
   record(Coll::SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl", bytes, t0);
   return work;
 }
@@ -1861,14 +1867,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     ipc(ds);
     icp = ds.ipc;
   }
-  const bool zx = zc_exchanges(ds, a, Coll::REDUCE_SCATTER, bytes);
-  auto work = gpu_run(Coll::REDUCE_SCATTER, ds, keep, {out}, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, out = out](hipStream_t x) mutable {
-      enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, *dsp, x, to);
-      if (!wo.is_same(out)) out.copy_(wo);
-    });
+  auto work = gpu_issue(Coll::REDUCE_SCATTER, ds, a, keep, {out}, to,
+                        [=, dsp = &ds, out = out](hipStream_t x) mutable {
+    enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, *dsp, x, to);
+    if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  note_zc(zx);
   record(Coll::REDUCE_SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
          bytes, t0);
   return work;
@@ -1920,15 +1923,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     ipc(ds);
     icp = ds.ipc;
   }
-  const bool zx = equal && zc_exchanges(ds, a, Coll::ALLTOALL, chunk);
-  auto work = gpu_run(Coll::ALLTOALL, ds, keep, outs, to, [&](hipStream_t s) {
-    ipc_issue(ds, a, s, zx, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
-      enqueue_alltoall(a, wi, wo, equal, *dsp, x, to);
-      for (size_t i = 0; i < outs.size(); ++i)
-        if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
-    });
+  auto work = gpu_issue(Coll::ALLTOALL, ds, a, keep, outs, to, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
+    enqueue_alltoall(a, wi, wo, equal, *dsp, x, to);
+    for (size_t i = 0; i < outs.size(); ++i)
+      if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
   }, icp);
-  note_zc(zx);
   record(Coll::ALLTOALL, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(chunk) ? "ipc_ll" : "ipc") : "rccl", total,
          t0);
   return work;

@@ -374,6 +374,7 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
       cfg_(Config::from_env()),
       health_(std::make_shared<Health>()) {
   members_key_ = make_members_key(global_ranks_, size);
+  if (const char* hp = std::getenv("PDCC_HOST_PROF")) hp_.on = *hp && *hp != '0';
   if (!cfg_.fault.empty()) {
     unsigned long long s = 0;
     char kind[32] = {0};
@@ -566,6 +567,13 @@ void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chr
   }
 }
 
+std::vector<std::tuple<std::string, uint64_t, double>> ProcessGroupMI355X::host_profile() {
+  static const char* kNames[] = {"before_op", "dev_state", "choose", "pre", "enqueue", "work", "record"};
+  std::vector<std::tuple<std::string, uint64_t, double>> out;
+  for (int i = 0; i < (int)HostStage::N; ++i) out.emplace_back(kNames[i], hp_.calls[i], hp_.ns[i] / 1e3);
+  return out;
+}
+
 std::vector<ProcessGroupMI355X::FrRecord> ProcessGroupMI355X::flight_recorder() {
   std::lock_guard<std::mutex> lk(stats_mu_);
   std::vector<FrRecord> out;
@@ -617,7 +625,6 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
-      << ", launcher_direct=" << (kv.second->launcher ? kv.second->launcher->direct : 0)
       << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0) << "}";
   o << ")";
   return o.str();
@@ -636,7 +643,7 @@ void ProcessGroupMI355X::abort_group(const std::string& why) {
         if (p.second->comm) p.second->comm->abort();
       }
       if (ds.ipc) ds.ipc->abort();  // kernels spinning in a cross-GPU barrier leave it
-      if (ds.launcher && ds.launcher->shm) ds.launcher->shm->abort();  // a job stuck in an exchange
+      if (ds.xchg) ds.xchg->abort();  // a launcher job (or an inline call) stuck in an exchange
     }
     if (shm_) shm_->abort();
   }
@@ -831,10 +838,12 @@ void ProcessGroupMI355X::p2p_submit(bool is_send, Job j) {
 // =================================================================== collectives
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce(std::vector<at::Tensor>& tensors,
                                                              const c10d::AllreduceOptions& opts) {
+  hp_.start();
   op_async_ = opts.asyncOp;
   check_single(tensors, "allreduce");
   at::Tensor& t = tensors[0];
   before_op(Coll::ALLREDUCE, tensors, -1);
+  hp_.lap(HostStage::BEFORE_OP);
   if (t.is_cuda()) return gpu_allreduce(t, opts.reduceOp.op_, -1, false, eff_timeout(opts.timeout));
   check_cpu_dtype(t.scalar_type(), opts.reduceOp.op_, "allreduce");
   const auto t0 = std::chrono::steady_clock::now();
@@ -1197,8 +1206,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::barrier(const c10d::BarrierOp
   }
   for (DeviceState* ds : dss) {
     const hipStream_t cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)ds->device).stream();
-    launcher_quiesce(*ds, cur);  // every launcher job launched (host), cur ordered behind them
-    if (ds->launcher) PDCC_HIP(hipStreamSynchronize(ds->launcher->zs->stream()));
+    launcher_quiesce(*ds);  // every zero-copy exchange published (gated kernels can finish)
     PDCC_HIP(hipStreamSynchronize(ds->stream.stream()));
     // synchronous collectives were enqueued on the caller's stream
     PDCC_HIP(hipStreamSynchronize(cur));

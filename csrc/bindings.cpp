@@ -47,7 +47,7 @@ pdcc::kern::RedOp kop(const std::string& s) {
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std::string& op, bool lds,
-                 int max_blocks) {
+                 int max_blocks, bool nt) {
   TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= pdcc::kern::kMaxRanks, "reduce_nway: 1..8 sources");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && al16(out.data_ptr()), "reduce_nway: out must be a contiguous, "
               "16-byte aligned GPU tensor");
@@ -64,9 +64,9 @@ void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(out.device().index()).stream();
   hipError_t e = lds ? pdcc::kern::reduce_nway(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
-                                               (int)srcs.size(), s, max_blocks)
+                                               (int)srcs.size(), s, max_blocks, nt)
                      : pdcc::kern::reduce_nway_regs(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
-                                                    (int)srcs.size(), s, max_blocks);
+                                                    (int)srcs.size(), s, max_blocks, nt);
   TORCH_CHECK(e == hipSuccess, "reduce_nway launch failed: ", hipGetErrorString(e));
 }
 
@@ -191,6 +191,15 @@ PYBIND11_MODULE(_C, m) {
       .def("healthy", &pdcc::ProcessGroupMI355X::healthy)
       .def("health_message", &pdcc::ProcessGroupMI355X::health_message)
       .def("set_algo", &pdcc::ProcessGroupMI355X::set_algo)
+      .def("host_profile",
+           [](pdcc::ProcessGroupMI355X& pg) {
+             py::dict d;
+             for (const auto& r : pg.host_profile())
+               d[py::str(std::get<0>(r))] = py::make_tuple(std::get<1>(r), std::get<2>(r));
+             return d;
+           },
+           "PDCC_HOST_PROF / set_host_profile(True): {stage: (calls, total_us)} of the GPU all_reduce host path")
+      .def("set_host_profile", &pdcc::ProcessGroupMI355X::set_host_profile, py::arg("on"))
       .def("set_ipc_thresholds", &pdcc::ProcessGroupMI355X::set_ipc_thresholds, py::arg("one_shot_max") = -1,
            py::arg("two_shot_max") = -1, py::arg("copy_max") = -1)
       .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>())
@@ -216,7 +225,8 @@ PYBIND11_MODULE(_C, m) {
       .def("log", &pdcc::IssueOrder::log);
 
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
-        py::arg("lds") = true, py::arg("max_blocks") = 0, "K1: out = op(srcs...) on the current stream");
+        py::arg("lds") = true, py::arg("max_blocks") = 0, py::arg("nt") = false,
+        "K1: out = op(srcs...) on the current stream (nt: non-temporal destination stores)");
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
         "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);

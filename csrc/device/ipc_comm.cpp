@@ -128,6 +128,11 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
     *err_host_ = 0;
     PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
+    PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&gates_host_), kern::kGateSlots * sizeof(kern::GateSlot),
+                           hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(gates_host_, 0, kern::kGateSlots * sizeof(kern::GateSlot));
+    PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&gates_dev_), gates_host_, 0));
+    gate_last_.assign(kern::kGateSlots, nullptr);
     if (const char* tr = std::getenv("PDCC_IPC_TRACE")) {
       const long n = std::atol(tr);
       if (n > 0) {
@@ -183,6 +188,8 @@ IpcComm::~IpcComm() {
       if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
     if (err_host_) hipHostFree(err_host_);
+    gate_last_.clear();
+    if (gates_host_) hipHostFree(gates_host_);
     if (trace_host_) hipHostFree(trace_host_);
   } catch (...) {
   }
@@ -276,6 +283,9 @@ void IpcComm::prepare_staging(const kern::IpcCall& call, hipStream_t stream) {
           "pdcc: this IPC collective needs more staging than the group has, and staging cannot grow while the "
           "stream is being captured into a graph: run the collective once before capturing it "
           "(parallel.graphs.capture does)");
+    if (tls_defer_frees_ && (need + kern::kTileBytes - 1) / kern::kTileBytes * kern::kTileBytes > cap_)
+      throw std::runtime_error("pdcc: an IPC launcher job needs " + std::to_string(need) + " B of staging, the group "
+                               "has " + std::to_string(cap_) + " (staging is grown by the submitting thread only)");
     ensure_staging(need, stream);
   }
   // A captured graph bakes the staging pointers into its kernel arguments: from
@@ -316,6 +326,7 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
 
 // ------------------------------------------------------------------ zero copy
 IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
+  std::lock_guard<std::mutex> zl(zc_mu_);
   ZcRec r{};
   zc_pending_ = false;
   if (!p && len == 0) {  // this rank has nothing the peers read (a scatter's non-root)
@@ -382,24 +393,29 @@ IpcComm::LaunchEvent::~LaunchEvent() {
 }
 
 void IpcComm::reap_closing(bool wait_all) {
-  std::lock_guard<std::mutex> lk(closing_mu_);
-  size_t keep = 0;
-  for (size_t i = 0; i < zc_closing_.size(); ++i) {
-    Closing& c = zc_closing_[i];
-    bool done = !c.last || !c.last->ev;
-    if (!done) {
-      const hipError_t e = wait_all ? hipEventSynchronize(c.last->ev) : hipEventQuery(c.last->ev);
-      done = e != hipErrorNotReady;
-      (void)hipGetLastError();
+  // pick the finished entries under the lock, close them outside it: a close synchronises
+  // the device, and the launcher's thread must stay free to queue more meanwhile
+  std::vector<Closing> done;
+  {
+    std::lock_guard<std::mutex> lk(closing_mu_);
+    size_t keep = 0;
+    for (size_t i = 0; i < zc_closing_.size(); ++i) {
+      Closing& c = zc_closing_[i];
+      bool fin = !c.last || !c.last->ev;
+      if (!fin) {
+        const hipError_t e = wait_all ? hipEventSynchronize(c.last->ev) : hipEventQuery(c.last->ev);
+        fin = e != hipErrorNotReady;
+        (void)hipGetLastError();
+      }
+      if (fin) done.push_back(std::move(c));
+      else zc_closing_[keep++] = std::move(c);
     }
-    if (done) {
-      if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
-      if (c.map) hipIpcCloseMemHandle(c.map);
-    } else {
-      zc_closing_[keep++] = std::move(c);
-    }
+    zc_closing_.resize(keep);
   }
-  zc_closing_.resize(keep);
+  for (auto& c : done) {
+    if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
+    if (c.map) hipIpcCloseMemHandle(c.map);
+  }
 }
 
 bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
@@ -454,6 +470,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
 }
 
 void IpcComm::zc_settle(bool ok) {
+  std::lock_guard<std::mutex> zl(zc_mu_);
   if (!zc_pending_) return;
   auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(),
                          [&](const ZcExport& e) { return e.id == zc_pending_id_; });
@@ -478,11 +495,55 @@ void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipS
   DeviceScope ds(device_);
   PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
   PDCC_HIP(hipEventRecord(le->ev, stream));
+  zc_note_launch(le);
+}
+
+void IpcComm::zc_note_launch(const std::shared_ptr<LaunchEvent>& le) {
   for (int r = 0; r < world_ && r < (int)zc_cur_ids_.size(); ++r) {
     if (r == rank_ || zc_cur_ids_[r] == 0) continue;
     for (auto& im : zc_imports_[r])
       if (im.id == zc_cur_ids_[r]) im.last = le;
   }
+}
+
+// ------------------------------------------------------------------ gated launches
+uint64_t IpcComm::gate_reserve() {
+  const uint64_t t = ++gate_next_;
+  auto& prev = gate_last_[t % kern::kGateSlots];
+  if (prev && prev->ev) {  // the launches of ticket t - kGateSlots read this slot
+    DeviceScope ds(device_);
+    if (hipEventQuery(prev->ev) == hipErrorNotReady) PDCC_HIP(hipEventSynchronize(prev->ev));
+    (void)hipGetLastError();
+  }
+  prev.reset();
+  return t;
+}
+
+void IpcComm::launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStream_t stream) {
+  call.zc = 0;
+  call.gate = gates_dev_ + (t % kern::kGateSlots);
+  call.gate_seq = t;
+  call.zoff = zoff;
+  prepare_staging(call, stream);  // (sized for either protocol, see ipc_staging_bytes)
+  launch_view(view(peer_staging_), call, stream);
+}
+
+std::shared_ptr<IpcComm::LaunchEvent> IpcComm::gate_mark(uint64_t t, hipStream_t stream) {
+  auto le = std::make_shared<LaunchEvent>();
+  DeviceScope ds(device_);
+  PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
+  PDCC_HIP(hipEventRecord(le->ev, stream));
+  gate_last_[t % kern::kGateSlots] = le;
+  return le;
+}
+
+void IpcComm::gate_publish(uint64_t t, bool ok, const std::vector<char*>& ptrs) {
+  kern::GateSlot* g = gates_host_ + (t % kern::kGateSlots);
+  volatile uint64_t* vp = g->ptr;
+  for (int r = 0; r < kern::kMaxRanks; ++r)
+    vp[r] = (ok && r < (int)ptrs.size()) ? reinterpret_cast<uint64_t>(ptrs[r]) : 0;
+  *reinterpret_cast<volatile uint32_t*>(&g->ok) = ok ? 1u : 0u;
+  __atomic_store_n(&g->seq, t, __ATOMIC_RELEASE);  // last: the kernels poll it
 }
 
 void IpcComm::maintain() {

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime_api.h>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -42,6 +43,11 @@ class IpcComm {
   // `bytes` fits. `stream` is drained before buffers are swapped.
   void ensure_staging(size_t bytes, hipStream_t stream);
   size_t max_staging() const { return max_staging_; }
+  size_t cap() const { return cap_; }
+  // Largest payload one launch may stage: on the IPC launcher's thread the staging it has
+  // (never grown there: growth frees and maps buffers, which synchronises the device while
+  // callers' streams wait on that thread -- the submitter primes it instead), else the cap.
+  size_t chunk_cap() const { return tls_defer_frees_ && cap_ > 0 ? std::min(max_staging_, cap_) : max_staging_; }
 
   // Launch one collective call (consumes one sequence number). May be captured
   // into a hipGraph once the staging is large enough for the call.
@@ -100,6 +106,22 @@ class IpcComm {
   void zc_settle(bool ok);
   // one zero-copy launch (call.zc is set here); bufs[r] = rank r's mapped buffer
   void launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream);
+
+  // ---- gated zero-copy launches (kern::GateSlot): launched before the exchange -------
+  // Next gate ticket (its slot is free: the launches that read the slot kGateSlots tickets
+  // ago have finished -- waits for them on the host in the rare case they have not).
+  uint64_t gate_reserve();
+  // One launch of `call` (the staged view; whole units), gated on ticket `t`; `zoff` = its
+  // byte offset inside every rank's buffer. Staging grows here (caller's thread) so the
+  // staged fallback fits.
+  void launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStream_t stream);
+  // after the launches of ticket `t`: their completion (slot reuse, mapping lifetime)
+  struct LaunchEvent;
+  std::shared_ptr<LaunchEvent> gate_mark(uint64_t t, hipStream_t stream);
+  // exchange thread: the mappings just imported are read by the launches of `ev`
+  void zc_note_launch(const std::shared_ptr<LaunchEvent>& ev);
+  // exchange thread: open ticket `t`'s gate (ok: ptrs[r] = rank r's mapped buffer)
+  void gate_publish(uint64_t t, bool ok, const std::vector<char*>& ptrs);
   size_t zc_exports() const { return zc_exports_.size(); }
   size_t zc_mappings() const;
   // evicted mappings not closed yet (their last launch may still run, or no safe point came)
@@ -133,11 +155,20 @@ class IpcComm {
     bool pinned;
     uint64_t last;  // LRU tick
   };
+  kern::GateSlot* gates_host_ = nullptr;  // pinned, device-mapped ring of kGateSlots
+  kern::GateSlot* gates_dev_ = nullptr;
+  uint64_t gate_next_ = 0;
+  std::vector<std::shared_ptr<LaunchEvent>> gate_last_;  // per slot: the launches that read it
+  std::mutex zc_mu_;  // zc_exports_ (the caller exports, the exchange thread settles)
+
+ public:
   // completion of one zero-copy launch (recorded on its stream right after it)
   struct LaunchEvent {
     hipEvent_t ev = nullptr;
     ~LaunchEvent();
   };
+
+ private:
   struct ZcImport {
     uint64_t id;
     void* map;  // hipIpcOpenMemHandle result (allocation base on this side)

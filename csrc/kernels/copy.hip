@@ -203,8 +203,11 @@ __device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c
 template <int W>
 __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
+  __shared__ IpcView sv;
+  __shared__ IpcCall sc;
   PhaseTrace tr(v);
-  ipc_copy_body<W>(v, c, lds, tr);
+  stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  ipc_copy_body<W>(sv, sc, lds, tr);
   tr.finish(v);
 }
 
@@ -234,7 +237,7 @@ static void canon(DType& t, RedOp& op) {
 }
 
 static hipError_t k1_dispatch(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
-                              int avg_div, hipStream_t stream, int max_blocks, bool lds) {
+                              int avg_div, hipStream_t stream, int max_blocks, int lds) {
   if (nsrc < 1 || nsrc > kMaxRanks || op == RedOp::COPY || !supports(t, op)) return hipErrorInvalidValue;
   canon(t, op);
   const size_t nbytes = count * dtype_size(t);
@@ -257,12 +260,12 @@ static hipError_t k1_dispatch(const void* const* srcs, int nsrc, void* out, size
 }
 
 hipError_t reduce_nway(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op, int avg_div,
-                       hipStream_t stream, int max_blocks) {
-  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, true);
+                       hipStream_t stream, int max_blocks, bool nt) {
+  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, 1 | (nt ? 2 : 0));
 }
 hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
-                            int avg_div, hipStream_t stream, int max_blocks) {
-  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, false);
+                            int avg_div, hipStream_t stream, int max_blocks, bool nt) {
+  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, nt ? 2 : 0);
 }
 
 // Default K2 grid from the launch's shape (scripts/k2_sweep.py on MI355X, profiles/README.md):
@@ -316,6 +319,14 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 size_t ipc_signal_bytes() { return kLLOffset + 2 * (size_t)kMaxRanks * kLLSlotBytes; }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
+  if (c.gate) {  // either protocol may run: the larger need
+    IpcCall z = c, st = c;
+    z.gate = st.gate = nullptr;
+    z.zc = 1;
+    st.zc = 0;
+    if (st.coll == IpcColl::ALLREDUCE_PUSH) st.coll = IpcColl::ALLREDUCE_2SHOT;
+    return std::max(ipc_staging_bytes(z, world), ipc_staging_bytes(st, world));
+  }
   if (c.zc)  // peers read the user buffers in place; a rooted reduce stages its reduced tiles,
              // the push all-reduce receives W slots of bytes / W
     return c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH
@@ -345,7 +356,8 @@ size_t ipc_staging_bytes(const IpcCall& c, int world) {
 hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream) {
   IpcCall c = call;
   if (v.world < 2 || v.world > kMaxRanks) return hipErrorInvalidValue;
-  if (c.zc) {  // in-place reads of user buffers: whole tiles (2-shot: whole rows of W tiles), no over-read
+  if (c.gate && (c.zc || is_ll(c.coll))) return hipErrorInvalidValue;  // the kernel picks zc for a gated call
+  if (c.zc || c.gate) {  // in-place reads of user buffers: whole tiles (2-shot: whole rows of W tiles), no over-read
     const bool rows = c.coll == IpcColl::ALLREDUCE_2SHOT || c.coll == IpcColl::BROADCAST_2SHOT ||
                       c.coll == IpcColl::REDUCE_2SHOT || c.coll == IpcColl::ALLREDUCE_PUSH;
     const bool known = rows || c.coll == IpcColl::ALLGATHER || c.coll == IpcColl::GATHER ||
@@ -385,7 +397,7 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   }
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);
-  if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc) return hipErrorInvalidValue;
+  if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc && !c.gate) return hipErrorInvalidValue;
   if (is_ll(c.coll) && (c.zc || c.bytes == 0 || c.bytes > kLLMaxBytes))
     return hipErrorInvalidValue;
   const bool ll_rooted = c.coll == IpcColl::REDUCE_LL || c.coll == IpcColl::BROADCAST_LL ||

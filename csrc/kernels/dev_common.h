@@ -192,7 +192,20 @@ __device__ __forceinline__ void wait_prologue(int i) {
 // NDST > 1: every reduced vector is stored to NDST destinations, m.dst(j, i) for
 // j < NDST (whole tiles only: the push all-reduce writes each owner's result into
 // every rank's tensor); the vmcnt accounting counts NDST stores per consume.
-template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int NDST = 1>
+// 16-B store; NT = non-temporal (global_store ... nt: streamed past the caches, for
+// destinations nobody re-reads soon)
+template <bool NT>
+__device__ __forceinline__ void store16(char* d, const uint4& r) {
+  if constexpr (NT) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {r.x, r.y, r.z, r.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(d));
+  } else {
+    *reinterpret_cast<uint4*>(d) = r;
+  }
+}
+
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int NDST = 1, bool NT = false>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   static_assert((DEPTH - 1) * (NSRC + NDST) < 64, "pipeline too deep for vmcnt");
   static_assert(DEPTH >= 2 && DEPTH <= 8, "prologue wait counts are written out for DEPTH <= 8");
@@ -229,7 +242,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
       char* d = m.dst(i);
       const size_t lim = m.valid(i);
       if (lane_off + 16 <= lim) {
-        *reinterpret_cast<uint4*>(d + lane_off) = r;
+        store16<NT>(d + lane_off, r);
       } else if (lane_off < lim) {
         store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
       }
@@ -276,7 +289,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
 
 // Register-staged engine (same Map contract): UNROLL tiles of NSRC vectors in
 // VGPRs per lane, no LDS. Kept for the A/B measurement against pipe_run.
-template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map>
+template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map, bool NT = false>
 __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -295,7 +308,7 @@ __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
       const uint4 r = reduce_vec<DT, OP, NSRC>(v[u], avg_div);
       char* d = m.dst(i + u);
       const size_t lim = m.valid(i + u);
-      if (lane_off + 16 <= lim) *reinterpret_cast<uint4*>(d + lane_off) = r;
+      if (lane_off + 16 <= lim) store16<NT>(d + lane_off, r);
       else if (lane_off < lim) store_partial(d + lane_off, r, (uint32_t)(lim - lane_off));
     }
   }
@@ -459,6 +472,53 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
   }
   __syncthreads();
   return ok;
+}
+
+// ----------------------------------------------------------------------------
+// Kernel arguments of the IPC kernels, staged once per block into LDS: a gated zero-copy
+// launch (kern::GateSlot) waits here until the host published the call's buffers, then
+// swaps them into the view (ok = 1) or falls back to the staged protocol (ok = 0, or the
+// wait gave up: error word set, the barriers that follow leave at once). Every block's
+// thread 0 polls the slot itself (no block waits for another block of the grid).
+__device__ __forceinline__ bool gate_wait(const kern::IpcView& v, const kern::IpcCall& c, uint32_t& ok) {
+  const kern::GateSlot* g = c.gate;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t it = 1;; ++it) {
+    if (__hip_atomic_load(&g->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == c.gate_seq) {
+      ok = __hip_atomic_load(&g->ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return true;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+      __hip_atomic_store(v.err, 0x400u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    if ((it & 15u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
+    // the slot is host memory: back off (a poll is a PCIe round trip), longer once the wait is long
+    if (it < 64) __builtin_amdgcn_s_sleep(4);
+    else __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+__device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, kern::IpcView& sv,
+                                           kern::IpcCall& sc) {
+  if (threadIdx.x == 0) {
+    sv = v;
+    sc = c;
+    if (c.gate) {
+      uint32_t ok = 0;
+      const bool live = gate_wait(v, c, ok);
+      if (live && ok) {
+        for (int r = 0; r < v.world; ++r)
+          sv.buf[r] = reinterpret_cast<char*>((uintptr_t)__hip_atomic_load(&c.gate->ptr[r], __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_SYSTEM)) + c.zoff;
+        sc.zc = 1;
+      } else {
+        sc.zc = 0;  // staged: the view's buffers are the staging windows already
+        if (sc.coll == kern::IpcColl::ALLREDUCE_PUSH) sc.coll = kern::IpcColl::ALLREDUCE_2SHOT;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 }  // namespace dev

@@ -49,11 +49,11 @@ bool supports(DType t, RedOp op);
 // AVG divides by `avg_div` (float types: multiply by 1/avg_div).
 // All pointers must be 16-byte aligned; count is in elements.
 hipError_t reduce_nway(const void* const* srcs, int nsrc, void* out, size_t count, DType t,
-                       RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0);
+                       RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0, bool nt = false);
 
 // register-staged variant of K1 (same numerics) kept for A/B measurement
 hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t count, DType t,
-                            RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0);
+                            RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0, bool nt = false);
 
 // ---------------------------------------------------------------- K2
 struct CopyDesc {
@@ -160,6 +160,20 @@ inline bool is_ll(IpcColl c) {
 // and every call whose last phase reads user buffers ends with a departure barrier
 // (no peer reads my buffer any more once my kernel is done, so the caller may
 // overwrite or free it).
+// Zero-copy gate. A gated launch (IpcCall::gate) is enqueued in stream order right away,
+// before the host has exchanged the call's buffer records with the peers; the kernel's
+// blocks wait (bounded spin) until the host's exchange thread publishes the slot: the
+// peers' mapped buffers (ok = 1: the zero-copy protocol) or ok = 0 (some rank could not
+// export or map: the same launch runs the staged protocol on its staging window).
+// Slots live in pinned host memory, one per in-flight gated call (ring of kGateSlots).
+struct GateSlot {
+  uint64_t seq;              // == IpcCall::gate_seq once `ok` and `ptr` are valid (written last)
+  uint32_t ok;
+  uint32_t pad;
+  uint64_t ptr[kMaxRanks];   // rank r's buffer of the call, mapped into this process (own: local)
+};
+constexpr int kGateSlots = 64;
+
 struct IpcCall {
   IpcColl coll;
   DType dtype;
@@ -173,6 +187,13 @@ struct IpcCall {
   size_t zstride;                // zero-copy chunked inputs: byte distance between chunks
   const void* in[kMaxRanks];     // local inputs: in[0] for single-tensor inputs, in[c] per chunk for lists
   void* out[kMaxRanks];          // local outputs: out[0] single, out[c] per chunk for lists
+  // gated zero-copy launch (see GateSlot): the slot (device-mapped host memory), the value
+  // its seq takes for this call, and this launch's byte offset inside every rank's buffer.
+  // The view passed with a gated call is the staged one (buf = staging); ok = 1 swaps in
+  // the slot's buffers (+ zoff) and runs the zero-copy protocol (zc = 1).
+  const GateSlot* gate;
+  uint64_t gate_seq;
+  size_t zoff;
 };
 
 // Bytes of staging needed for `call` (padded to tiles).

@@ -17,6 +17,7 @@ using kern::IpcView;
 struct Ptrs8 {
   const char* p[kern::kMaxRanks];
   int chunked;  // K1 tile->block map: 0 = strided (block b: b, b+G, ...), 1 = contiguous run per block
+  int nt;       // K1 destination stores non-temporal (global_store ... nt)
 };
 
 // LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU)
@@ -74,14 +75,16 @@ template <DType DT, RedOp OP, int NSRC, int D>
 __global__ void __launch_bounds__(256) k1_reduce_lds(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<NSRC, D>::kBytes];
   const StridedMap m = k1_map(srcs, dst, nbytes);
-  pipe_run<DT, OP, NSRC, D>(lds, m, avg_div);
+  if (srcs.nt) pipe_run<DT, OP, NSRC, D, StridedMap, 1, true>(lds, m, avg_div);
+  else pipe_run<DT, OP, NSRC, D>(lds, m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
 
 template <DType DT, RedOp OP, int NSRC>
 __global__ void __launch_bounds__(256) k1_reduce_regs(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
   const StridedMap m = k1_map(srcs, dst, nbytes);
-  pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2)>(m, avg_div);
+  if (srcs.nt) pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2), StridedMap, true>(m, avg_div);
+  else pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2)>(m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
 
@@ -416,8 +419,11 @@ __device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall&
 template <DType DT, RedOp OP, int W>
 __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, DepthFor<W>::value>::kBytes];
+  __shared__ IpcView sv;
+  __shared__ IpcCall sc;
   PhaseTrace tr(v);
-  ipc_reduce_body<DT, OP, W>(v, c, lds, tr);
+  stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);
   tr.finish(v);
 }
 
@@ -727,7 +733,7 @@ __global__ void __launch_bounds__(256) k_ll_alltoall(IpcView v, IpcCall c) {
 // host-side dispatch, one pair of functions per dtype (defined in reduce_<dt>.hip)
 #define PDCC_DECL_DISPATCH(DTNAME)                                                                   \
   hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,    \
-                                  int avg_div, hipStream_t s, int grid, bool lds);                   \
+                                  int avg_div, hipStream_t s, int grid, int lds);                    \
   hipError_t ipc_dispatch_##DTNAME(const IpcView& v, const IpcCall& c, hipStream_t s, int grid);
 PDCC_DECL_DISPATCH(F32)
 PDCC_DECL_DISPATCH(F16)
@@ -739,9 +745,10 @@ PDCC_DECL_DISPATCH(I32)
 PDCC_DECL_DISPATCH(I64)
 #undef PDCC_DECL_DISPATCH
 
+// `mode`: bit 0 = LDS-DMA engine (else registers), bit 1 = non-temporal stores
 template <DType DT, RedOp OP, int NSRC>
 hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_div, hipStream_t s, int grid,
-                     bool lds) {
+                     int mode) {
   Ptrs8 p{};
   for (int k = 0; k < NSRC; ++k) p.p[k] = (const char*)srcs[k];
   static const int chunked = [] {
@@ -749,6 +756,8 @@ hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_
     return e && *e == '1' ? 1 : 0;
   }();
   p.chunked = chunked;
+  p.nt = (mode & 2) ? 1 : 0;
+  const bool lds = (mode & 1) != 0;
   if (lds)
     hipLaunchKernelGGL((k1_reduce_lds<DT, OP, NSRC, K1Deep<NSRC>::value>), dim3(grid), dim3(256), 0, s, p, (char*)out,
                        nbytes, avg_div);
@@ -759,7 +768,7 @@ hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_
 
 template <DType DT, RedOp OP>
 hipError_t k1_by_n(const void* const* srcs, int n, void* out, size_t nbytes, int avg_div, hipStream_t s, int grid,
-                   bool lds) {
+                   int lds) {
   switch (n) {
     case 1: return launch_k1<DT, OP, 1>(srcs, out, nbytes, avg_div, s, grid, lds);
     case 2: return launch_k1<DT, OP, 2>(srcs, out, nbytes, avg_div, s, grid, lds);
@@ -836,7 +845,7 @@ hipError_t ipc_by_w(const IpcView& v, const IpcCall& c, hipStream_t s, int grid)
   namespace pdcc {                                                                                    \
   namespace dev {                                                                                     \
   hipError_t k1_dispatch_##DTNAME(const void* const* srcs, int n, void* out, size_t nb, RedOp op,     \
-                                  int avg_div, hipStream_t s, int grid, bool lds) {                   \
+                                  int avg_div, hipStream_t s, int grid, int lds) {                    \
     constexpr DType DT = DType::DTNAME;                                                               \
     switch (op) { OPSET(k1_by_n, srcs, n, out, nb, avg_div, s, grid, lds) default: return hipErrorInvalidValue; } \
   }                                                                                                   \

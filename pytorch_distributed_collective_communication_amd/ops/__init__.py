@@ -4,7 +4,8 @@
   same-shaped GPU tensors; ``op`` in sum/avg/prod/min/max (+ band/bor/bxor for
   integers). Default implementation stages tiles through LDS with
   ``global_load_lds_dwordx4`` (LDS-DMA ring); ``impl="regs"`` is the
-  register-staged variant kept for A/B measurement.
+  register-staged variant kept for A/B measurement; a ``_nt`` suffix
+  (``"lds_nt"``, ``"regs_nt"``) makes the destination stores non-temporal.
 * :func:`multi_copy`, :func:`pack`, :func:`unpack` -- K2: one launch copies a
   whole list of tensors (the staging used by gather/scatter/all_gather with
   tensor lists, reference main.py:35-37,51-52,66-68).
@@ -33,12 +34,14 @@ def reduce_nway(srcs: Sequence[torch.Tensor], out: torch.Tensor | None = None, o
     """K1 N-way element-wise reduction on the GPU (1 <= len(srcs) <= 8)."""
     if op not in _OPS:
         raise ValueError(f"op must be one of {_OPS}, got {op!r}")
+    if impl not in ("lds", "regs", "lds_nt", "regs_nt"):
+        raise ValueError(f"impl must be lds|regs|lds_nt|regs_nt, got {impl!r}")
     srcs = list(srcs)
     if not srcs:
         raise ValueError("reduce_nway needs at least one source")
     if out is None:
         out = torch.empty_like(srcs[0], memory_format=torch.contiguous_format)
-    _C().reduce_nway(srcs, out, op, impl != "regs", int(max_blocks))
+    _C().reduce_nway(srcs, out, op, not impl.startswith("regs"), int(max_blocks), impl.endswith("_nt"))
     return out
 
 

@@ -58,6 +58,12 @@ for s in "$@"; do
         --env PDCC_ALGO=ipc PDCC_IPC_ZC_CACHE=4 PDCC_IPC_1SHOT_MAX=256K ;;
     atsdebug) step atsdebug 150 python scripts/zc_debug.py async_then_sync --world 2 --dump-s 40 \
         --env PDCC_ALGO=ipc ;;
+    zcasyncbench) step zcasyncbench 300 python scripts/zc_async_bench.py ;;
+    churntrace) step churntrace 400 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --hip-trace --stats --output-format csv \
+        -d "$0/gpurun_out/prof_churn" -o churn_%pid% -- python3 "$0/scripts/zc_async_bench.py" --churn' "$(pwd)" ;;
+    hostpath) step hostpath 300 python scripts/host_path_bench.py ;;
+    tgdebug) step tgdebug 150 python scripts/zc_debug.py two_groups --world 2 --dump-s 40 --env PDCC_ALGO=ipc ;;
+    k1sweep) step k1sweep 300 python scripts/k1_sweep.py ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Where the host time of one small GPU all_reduce goes (verdict r2 weak #6).
+
+Two ranks share the GPU (PDCC_ALGO=ipc). Per case, `--calls` back-to-back
+dist.all_reduce calls with the backend's stage profiler on (PDCC_HOST_PROF):
+  py_call_us   -- host time of the Python call (dist.all_reduce returns), median
+  per_call_us  -- wall time per call of the back-to-back loop incl. the GPU (max over ranks)
+  stages_us    -- mean per call of each C++ stage (before_op, dev_state, choose, pre,
+                  enqueue, work, record), and `c10d_python` = py_call - sum(stages)
+Cases: 4 B (LL kernel), 64 KiB (LL), 4 MiB async (zero-copy job on the IPC launcher).
+
+    python scripts/host_path_bench.py [--calls 2000]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def work(rank, size, calls):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    b = be.native_backend(None, "cuda")
+    out = {}
+    for name, nbytes, async_op in (("4B", 4, False), ("64KiB", 64 << 10, False), ("4MiB_async", 4 << 20, True)):
+        x = torch.full((max(1, nbytes // 4),), 1.0, device=dev)
+        for _ in range(50):
+            w = dist.all_reduce(x, async_op=async_op)
+        torch.cuda.synchronize()
+        dist.barrier()
+        b.set_host_profile(True)
+        host = []
+        k = calls if nbytes <= (64 << 10) else calls // 10
+        t0 = time.perf_counter()
+        for _ in range(k):
+            h0 = time.perf_counter()
+            w = dist.all_reduce(x, async_op=async_op)
+            host.append(time.perf_counter() - h0)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / k
+        algo = b.last_algo()
+        prof = b.host_profile()
+        b.set_host_profile(False)
+        stages = {s: (tot / max(1, n)) for s, (n, tot) in prof.items()}
+        py = statistics.median(host) * 1e6
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out[name] = {"algo": algo, "py_call_us": round(py, 2), "per_call_us": round(t.item() * 1e6, 2),
+                     "stages_us": {s: round(v, 2) for s, v in stages.items()},
+                     "c10d_python_us": round(py - sum(stages.values()), 2)}
+        x.fill_(1.0)
+        dist.all_reduce(x)
+        out[name]["correct"] = bool(torch.all(x == size).item())
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=2000)
+    ap.add_argument("--world", type=int, default=2)
+    a = ap.parse_args()
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+
+    res = launch(work, a.world, args=(a.calls,), bind_device=True, timeout_s=60, env={"PDCC_ALGO": "ipc"},
+                 join_timeout_s=300)
+    for name, r in res[0].items():
+        print(json.dumps({"world_on_one_gpu": a.world, "case": name, **r}), flush=True)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """K1 tuning sweep (interleaved rounds in one process): grid size x engine for
-2/4/8-source fp32 reduces of 256 MiB per source, plus torch baselines."""
+2/4/8-source fp32 reduces of 256 MiB per source (LDS-DMA / register engines, normal /
+non-temporal stores), plus torch baselines."""
 import json
 import os
 import statistics
@@ -31,13 +32,16 @@ for nsrc in (2, 4, 8):
     dst = torch.empty_like(srcs[0])
     res = {}
     for _ in range(4):
-        for impl in ("lds", "regs"):
-            for g in (256, 512):
+        for impl in ("lds", "regs", "lds_nt", "regs_nt"):
+            for g in (256, 512, 1024):
                 t = timeit(lambda: ops.reduce_nway(srcs, out=dst, impl=impl, max_blocks=g))
                 res.setdefault(f"n{nsrc}_{impl}_g{g}", []).append((nsrc + 1) * n * 4 / t / 1e9)
         if nsrc == 2:
             t = timeit(lambda: torch.add(srcs[0], srcs[1], out=dst))
             res.setdefault("n2_torch_add", []).append(3 * n * 4 / t / 1e9)
+        else:
+            t = timeit(lambda: torch.sum(torch.stack(srcs), 0, out=dst))
+            res.setdefault(f"n{nsrc}_torch_stack_sum", []).append((nsrc + 1) * n * 4 / t / 1e9)
     for k, v in res.items():
         out[k] = round(statistics.median(v), 1)
     del srcs, dst

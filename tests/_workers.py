@@ -1384,10 +1384,12 @@ def zc_async_probe(rank, size, device="cuda", trials=5, n=16 << 20, late_ms=50):
     return res
 
 
-def zc_churn_probe(rank, size, device="cuda", allocs=40, n=(1 << 20) // 4 + 64):
-    """More distinct >= 1 MiB allocations than the zero-copy cache holds: exports get
-    evicted and their mappings closed once the last launch that read them is done (no
-    device-wide sync); every result right, the closing list drains."""
+def zc_churn_probe(rank, size, device="cuda", allocs=40, n=(10 << 20) // 4 + 64):
+    """More distinct allocations than the zero-copy cache holds (10 MiB each: every one
+    its own caching-allocator segment): exports get evicted and their mappings closed
+    once the last launch that read them is done (no device-wide sync: this probe itself
+    only synchronises its stream, so a hipDeviceSynchronize in a trace would be the
+    library's); every result right, the closing list drains at the barrier."""
     import torch
     import torch.distributed as dist
 
@@ -1403,11 +1405,38 @@ def zc_churn_probe(rank, size, device="cuda", allocs=40, n=(1 << 20) // 4 + 64):
             w = dist.all_reduce(t, async_op=True)
             if i % 3 == 0:
                 w.wait()
-        torch.cuda.synchronize()
+        torch.cuda.current_stream().synchronize()
         for i, t in enumerate(bufs):
             ok = ok and bool(torch.all(t == sum(r + i for r in range(size))))
-    dist.barrier()
+    before = b.describe()
+    dist.barrier()  # releases what the launcher's thread queued (evicted mappings)
     x = torch.ones(n, device=d)
-    dist.all_reduce(x)  # one more exchange: reaps what finished
+    dist.all_reduce(x)
+    torch.cuda.current_stream().synchronize()
+    return {"ok": ok, "algo": b.last_algo(), "desc": b.describe(), "before_barrier": before}
+
+
+def zc_burst_probe(rank, size, device="cuda", calls=64, n=(4 << 20) // 4):
+    """A burst of async zero-copy all_reduces (no wait()), then torch.cuda.synchronize(),
+    then the tensors are refilled and reduced once more synchronously: every result exact
+    (a kernel launched after the synchronize would corrupt the refilled data)."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    bufs = [torch.full((n,), float(rank + 1 + i % 3), device=d) for i in range(4)]
+    for i in range(calls):
+        dist.all_reduce(bufs[i % 4], async_op=True)
     torch.cuda.synchronize()
-    return {"ok": ok, "algo": b.last_algo(), "desc": b.describe()}
+    ok = {}
+    for i, b in enumerate(bufs):
+        k = len(range(i, calls, 4))  # reductions this buffer got
+        want = sum(r + 1 + i % 3 for r in range(size)) * size ** (k - 1)
+        ok[f"burst{i}"] = bool(torch.all(b == want).item())
+    for i, b in enumerate(bufs):
+        b.fill_(float(rank + 1))
+        dist.all_reduce(b)
+    torch.cuda.synchronize()
+    for i, b in enumerate(bufs):
+        ok[f"after{i}"] = bool(torch.all(b == size * (size + 1) / 2).item())
+    return ok
