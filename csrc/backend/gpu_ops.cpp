@@ -914,9 +914,10 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
     if (!selftest) launcher_quiesce(ds);  // inline exchange: the channel is this thread's now
     body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
   }
-  {
+  if (!selftest) {  // recorded as zero-copy if this rank shares its buffer (a gated call whose
+                   // exchange fails on another rank runs staged: describe() "zc_fallbacks")
     std::lock_guard<std::mutex> lk(stats_mu_);
-    zc_ran_ = body > 0;
+    zc_ran_ = body > 0 && (zbuf != nullptr || zlen == 0);
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;

@@ -64,6 +64,11 @@ for s in "$@"; do
     hostpath) step hostpath 300 python scripts/host_path_bench.py ;;
     tgdebug) step tgdebug 150 python scripts/zc_debug.py two_groups --world 2 --dump-s 40 --env PDCC_ALGO=ipc ;;
     k1sweep) step k1sweep 300 python scripts/k1_sweep.py ;;
+    gpuA) step gpuA 1100 python -u -m pytest tests/test_backend_gpu.py -v --timeout 300 --timeout-method thread ;;
+    gpuB) step gpuB 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        --deselect tests/test_backend_gpu.py ;;
+    gpuA2) step gpuA2 600 python -u -m pytest tests/test_backend_gpu.py -v --timeout 300 --timeout-method thread \
+        -k "world8 or list_all_to_all or conformance or ll_reduce_scatter" ;;
     bench2shared) PDCC_BENCH_SMALL=1 step bench2shared 600 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 \
         --bytes 67108864 ;;
