@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 // Zero-copy copies (IpcCall::zc): peers' user buffers are read in place; data
 // arrival barrier first, departure barrier last (see ipc_reduce_zc).
 template <int W>
-__device__ __forceinline__ void ipc_copy_zc(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr,
+__device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                             uint32_t ep) {
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void ipc_copy_zc(const IpcView& v, const IpcCall& c, 
 }
 
 template <int W>
-__device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
+__device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr) {
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
   const uint32_t seq = block_seq(v);
@@ -203,8 +203,8 @@ __device__ __forceinline__ void ipc_copy_body(const IpcView& v, const IpcCall& c
 template <int W>
 __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
-  __shared__ IpcView sv;
-  __shared__ IpcCall sc;
+  __shared__ DView sv;
+  __shared__ DCall sc;
   PhaseTrace tr(v);
   stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
   ipc_copy_body<W>(sv, sc, lds, tr);

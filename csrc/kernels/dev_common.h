@@ -32,6 +32,26 @@ constexpr int kTile = kern::kTileBytes;
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) const void gbl_cvoid_t;
 
+// A pointer known to be global (address space 1) that converts to a plain one where it
+// is used: the conversion is an addrspacecast the compiler sees through, so loads and
+// stores through it stay global_* instructions even when the pointer itself was read
+// from LDS (a plain pointer read from LDS is generic: flat_* accesses).
+template <class T>
+struct gp {
+  __attribute__((address_space(1))) T* p;
+  __device__ __forceinline__ operator T*() const { return (T*)p; }
+  template <class U>
+  __device__ __forceinline__ explicit operator U*() const { return (U*)(T*)p; }
+  __device__ __forceinline__ gp& operator=(T* q) {
+    p = (__attribute__((address_space(1))) T*)q;
+    return *this;
+  }
+};
+using DView = kern::IpcViewT<gp>;  // the IPC kernels' arguments, staged in LDS
+using DCall = kern::IpcCallT<gp>;
+static_assert(sizeof(DView) == sizeof(kern::IpcView) && sizeof(DCall) == sizeof(kern::IpcCall),
+              "device and host argument layouts differ");
+
 // ----------------------------------------------------------------------------
 // waits
 template <int N>
@@ -360,7 +380,8 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
 // counters[b], and consecutive launches on a stream run in order, so relaxed
 // accesses suffice (uncached signal memory: no stale line on any XCD); the store
 // is drained by the arrival barrier that follows.
-__device__ __forceinline__ uint32_t block_seq(const kern::IpcView& v) {
+template <class V>
+__device__ __forceinline__ uint32_t block_seq(const V& v) {
   __shared__ uint32_t s_seq;
   if (threadIdx.x == 0) {
     uint32_t* const c = v.counters + blockIdx.x;
@@ -427,8 +448,8 @@ __device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
 // order) that every peer's previous kernel has finished and no longer reads the
 // staging this call is about to overwrite. Returns false on timeout (error word
 // set, block continues so the grid always drains).
-template <bool DATA = true>
-__device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t value) {
+template <bool DATA = true, class V>
+__device__ __forceinline__ bool block_barrier(const V& v, uint32_t value) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   drain_vm();       // every storing wave drains its stores
@@ -453,13 +474,13 @@ __device__ __forceinline__ bool block_barrier(const kern::IpcView& v, uint32_t v
       if (__all(me_ok)) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
         if (lane == 0)
-          __hip_atomic_store(v.err, 0x100u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(static_cast<uint32_t*>(v.err), 0x100u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = false;
         break;
       }
       // every 256 polls: has the host aborted the group (IpcComm::abort), or did
       // another block already time out? Either way stop waiting, so the grid drains.
-      if ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+      if ((it & 255u) == 0 && __hip_atomic_load(static_cast<uint32_t*>(v.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
         ok = false;
         break;
       }
@@ -489,21 +510,20 @@ __device__ __forceinline__ bool gate_wait(const kern::IpcView& v, const kern::Ip
       return true;
     }
     if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
-      __hip_atomic_store(v.err, 0x400u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(static_cast<uint32_t*>(v.err), 0x400u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
-    if ((it & 15u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
+    if ((it & 15u) == 0 && __hip_atomic_load(static_cast<uint32_t*>(v.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
     // the slot is host memory: back off (a poll is a PCIe round trip), longer once the wait is long
     if (it < 64) __builtin_amdgcn_s_sleep(4);
     else __builtin_amdgcn_s_sleep(127);
   }
 }
 
-__device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, kern::IpcView& sv,
-                                           kern::IpcCall& sc) {
+__device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, DView& sv, DCall& sc) {
   if (threadIdx.x == 0) {
-    sv = v;
-    sc = c;
+    __builtin_memcpy(&sv, &v, sizeof(DView));  // same layout, pointers retyped global
+    __builtin_memcpy(&sc, &c, sizeof(DCall));
     if (c.gate) {
       uint32_t ok = 0;
       const bool live = gate_wait(v, c, ok);

@@ -91,19 +91,29 @@ constexpr size_t kLLOffset = 40960;                        // byte offset of the
 constexpr size_t kLLMaxBytes = 64u << 10;                  // payload per rank of one LL call
 constexpr size_t kLLSlotBytes = 2 * kLLMaxBytes;           // 8-byte words of 4 data bytes
 static_assert(kLLOffset >= (size_t)(kLLCtlWord + 16) * 4, "LL slots overlap the signal words");
-struct IpcView {
-  char* buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes; zero-copy: user buffers
-  char* stg[kMaxRanks];        // staging buffer per rank (zero-copy calls that still stage results)
-  uint32_t* flags[kMaxRanks];  // signal area (uncached device memory) per rank
-  uint32_t* err;               // host-mapped error word (0 = ok), written on spin timeout
-  uint32_t* counters;          // own signal area + kCountWord: per-block call counters
-  size_t cap;                  // staging bytes
+// The view and call structs are templates over the pointer type P<T>: the host (and the
+// kernel arguments) use plain pointers (IpcView / IpcCall); the IPC kernels copy their
+// arguments into LDS as dev::DView / dev::DCall, whose pointers are typed global
+// (address space 1) -- a plain pointer read back from LDS is a generic one, and every
+// access through it would be a flat instruction. Same layout either way.
+template <class T>
+using RawPtr = T*;
+
+template <template <class> class P>
+struct IpcViewT {
+  P<char> buf[kMaxRanks];        // staging buffer per rank (own included), `cap` bytes; zero-copy: user buffers
+  P<char> stg[kMaxRanks];        // staging buffer per rank (zero-copy calls that still stage results)
+  P<uint32_t> flags[kMaxRanks];  // signal area (uncached device memory) per rank
+  P<uint32_t> err;               // host-mapped error word (0 = ok), written on spin timeout
+  P<uint32_t> counters;          // own signal area + kCountWord: per-block call counters
+  size_t cap;                    // staging bytes
   int rank;
   int world;
-  uint64_t timeout_ticks;      // s_memrealtime ticks (100 MHz) before a spin gives up
-  uint64_t* trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
-  uint32_t trace_cap;          // records in the ring
+  uint64_t timeout_ticks;        // s_memrealtime ticks (100 MHz) before a spin gives up
+  P<uint64_t> trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
+  uint32_t trace_cap;            // records in the ring
 };
+using IpcView = IpcViewT<RawPtr>;
 
 // Device-side phase trace of an IPC call (block 0, s_memrealtime ticks at 100 MHz):
 // [0] block 0's call number, [1] entry, [2] arrival barrier passed, [3] local data
@@ -174,7 +184,8 @@ struct GateSlot {
 };
 constexpr int kGateSlots = 64;
 
-struct IpcCall {
+template <template <class> class P>
+struct IpcCallT {
   IpcColl coll;
   DType dtype;
   RedOp op;
@@ -185,16 +196,17 @@ struct IpcCall {
   int zc;                        // 1 = zero-copy call (see above)
   size_t bytes;                  // payload bytes (per rank / per chunk, see above)
   size_t zstride;                // zero-copy chunked inputs: byte distance between chunks
-  const void* in[kMaxRanks];     // local inputs: in[0] for single-tensor inputs, in[c] per chunk for lists
-  void* out[kMaxRanks];          // local outputs: out[0] single, out[c] per chunk for lists
+  P<const void> in[kMaxRanks];   // local inputs: in[0] for single-tensor inputs, in[c] per chunk for lists
+  P<void> out[kMaxRanks];        // local outputs: out[0] single, out[c] per chunk for lists
   // gated zero-copy launch (see GateSlot): the slot (device-mapped host memory), the value
   // its seq takes for this call, and this launch's byte offset inside every rank's buffer.
   // The view passed with a gated call is the staged one (buf = staging); ok = 1 swaps in
   // the slot's buffers (+ zoff) and runs the zero-copy protocol (zc = 1).
-  const GateSlot* gate;
+  P<const GateSlot> gate;
   uint64_t gate_seq;
   size_t zoff;
 };
+using IpcCall = IpcCallT<RawPtr>;
 
 // Bytes of staging needed for `call` (padded to tiles).
 size_t ipc_staging_bytes(const IpcCall& call, int world);

@@ -98,7 +98,7 @@ __device__ __forceinline__ size_t pad_tiles(size_t b) { return (b + kTile - 1) /
 
 template <int W>
 struct AllSrcMap {  // reduce tile t of every rank's staging (+ chunk offset)
-  const IpcView* v;
+  const DView* v;
   size_t base;   // byte offset of the chunk inside each staging buffer
   char* d;       // destination (user output or own staging)
   size_t dlim;   // bytes writable at d (user: payload bytes; staging: padded)
@@ -140,7 +140,7 @@ constexpr int kCopyDepth = 4;
 // (staging is sized to whole rows, see kern::ipc_staging_bytes); valid() = 0 there.
 template <int W>
 struct OwnerRowMap {
-  char* const* bufs;  // the owners' buffers (IpcView::buf, or ::stg for a zero-copy reduce)
+  const gp<char>* bufs;  // the owners' buffers (IpcView::buf, or ::stg for a zero-copy reduce)
   size_t poff;  // offset of this call in the staging buffers (0: one buffer)
   char* d;
   size_t dlim;
@@ -173,7 +173,7 @@ struct OwnerRowMap {
 // stride*k, owners rotated per item, row and block like OwnerRowMap. Rows are whole.
 template <int W>
 struct PeerRowMap {
-  const IpcView* v;
+  const DView* v;
   char* d;
   uint32_t rot;
   size_t first, stride, nrows;
@@ -201,7 +201,7 @@ struct PeerRowMap {
 template <int W>
 struct PushMap {
   const char* mine;   // my tensor
-  char* const* stgs;  // every rank's staging (IpcView::stg)
+  const gp<char>* stgs;  // every rank's staging (IpcView::stg)
   int me;
   uint32_t rot;
   size_t first, stride, nrows;
@@ -229,7 +229,7 @@ struct PushMap {
 // owner's bits), stored into every rank's tensor (destination j = rank j).
 template <int W>
 struct PushReduceMap {
-  char* const* bufs;  // every rank's tensor (IpcView::buf)
+  const gp<char>* bufs;  // every rank's tensor (IpcView::buf)
   const char* stg;    // my staging (slot s, row r at (s * nrows + r) * kTile)
   int me;
   size_t first, stride, nrows;
@@ -248,8 +248,8 @@ struct PushReduceMap {
 // source q's tile lives at v->buf[q] + sbase + t*kTile and lands in out[q].
 template <int W>
 struct PeerTileMap {
-  const IpcView* v;
-  const IpcCall* c;
+  const DView* v;
+  const DCall* c;
   size_t sbase;  // offset of the chunk inside each staging buffer
   size_t dlim;
   uint32_t rot;
@@ -284,7 +284,7 @@ struct PeerTileMap {
 // Phase 1 of the all-reduce writes the reduced own tiles in place: peers only ever
 // read tiles they own there, and those are not written by this rank.
 template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_reduce_zc(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr,
+__device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                               uint32_t ep) {
   constexpr int D = DepthFor<W>::value;
   const size_t G = gridDim.x, b = blockIdx.x;
@@ -347,7 +347,7 @@ __device__ __forceinline__ void ipc_reduce_zc(const IpcView& v, const IpcCall& c
 }
 
 template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall& c, char* lds, const PhaseTrace tr) {
+__device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr) {
   constexpr int D = DepthFor<W>::value;
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
@@ -419,8 +419,8 @@ __device__ __forceinline__ void ipc_reduce_body(const IpcView& v, const IpcCall&
 template <DType DT, RedOp OP, int W>
 __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, DepthFor<W>::value>::kBytes];
-  __shared__ IpcView sv;
-  __shared__ IpcCall sc;
+  __shared__ DView sv;
+  __shared__ DCall sc;
   PhaseTrace tr(v);
   stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
   ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);

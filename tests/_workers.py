@@ -1440,3 +1440,46 @@ def zc_burst_probe(rank, size, device="cuda", calls=64, n=(4 << 20) // 4):
     for i, b in enumerate(bufs):
         ok[f"after{i}"] = bool(torch.all(b == size * (size + 1) / 2).item())
     return ok
+
+
+# elements per case: every size ragged (not a multiple of a 4 KiB tile or of W tiles)
+_NUMERICS_SIZES = {"ll": (1, 777, 16381), "oneshot": (40_009, 100_003), "twoshot": (300_007, 1_000_003),
+                   "zc": (700_001, 2_000_003), "push": (700_001, 2_000_003)}
+
+
+def random_numerics(rank, size, device="cuda", mode="ll"):
+    """Seeded random fp32 / bf16 / fp16 all_reduce (SUM / AVG / PRODUCT / MAX / MIN) and
+    reduce_scatter (SUM) through ONE IPC protocol -- picked by the test's environment --
+    against an fp64 torch reduction of every rank's input (each rank regenerates all of
+    them; utils/conformance.py `_close`: MAX/MIN bitwise, SUM/AVG within (W+1) eps of
+    sum|x|, PRODUCT within (W+1) eps of |prod|). Reference call sites: main.py:14-15,23-24.
+    Returns {case: [ok, engine]}."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+    from pytorch_distributed_collective_communication_amd.utils.conformance import _close, _seeded
+
+    d = _dev(device)
+    gb = be.native_backend(None, "cuda")
+    out = {}
+    dts = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
+    for dtn, dt in dts.items():
+        for n in _NUMERICS_SIZES[mode]:
+            for k, op in enumerate(("SUM", "AVG", "PRODUCT", "MAX", "MIN")):
+                lo, hi = (0.5, 1.5) if op == "PRODUCT" else (-1.0, 1.0)
+                seed = 1000 * k + n % 997
+                xs = [_seeded((n,), dt, seed + 31 * r, d, lo, hi) for r in range(size)]
+                t = xs[rank].clone()
+                dist.all_reduce(t, op=getattr(dist.ReduceOp, op))
+                out[f"all_reduce/{dtn}/{op}/{n}"] = [_close(t.cpu(), [x.cpu() for x in xs], op, size, dtn),
+                                                     gb.last_algo()]
+            # reduce_scatter of W ragged chunks (chunk sizes follow the same protocol thresholds / W)
+            m = max(1, n // size)
+            xs = [_seeded((size * m,), dt, 77 + n % 991 + 31 * r, d) for r in range(size)]
+            o = torch.empty(m, dtype=dt, device=d)
+            dist.reduce_scatter_tensor(o, xs[rank].clone())
+            mine = [x[rank * m:(rank + 1) * m].cpu() for x in xs]
+            out[f"reduce_scatter/{dtn}/SUM/{m}"] = [_close(o.cpu(), mine, "SUM", size, dtn), gb.last_algo()]
+    dist.barrier()
+    return out

@@ -438,3 +438,30 @@ def test_zero_copy_eviction_churn(cache):
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": cache}
     for r in _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120):
         assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+
+
+# verdict r2 #6: random-data numerics of every IPC protocol through the collective API,
+# against an fp64 torch reference (not another engine); the environment forces one protocol
+_NUMERICS_ENV = {
+    "ll": ({"PDCC_ALGO": "ipc"}, "ipc_ll"),
+    "oneshot": ({"PDCC_ALGO": "ipc", "PDCC_IPC_LL_MAX": "0", "PDCC_IPC_ZC": "0"}, "ipc_1shot"),
+    "twoshot": ({"PDCC_ALGO": "ipc", "PDCC_IPC_LL_MAX": "0", "PDCC_IPC_ZC": "0", "PDCC_IPC_1SHOT_MAX": "64K"},
+                "ipc_2shot"),
+    "zc": ({"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_2shot_zc"),
+    "push": ({"PDCC_ALGO": "ipc_push", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_push"),
+}
+
+
+@pytest.mark.parametrize("mode", list(_NUMERICS_ENV))
+@pytest.mark.parametrize("world", [2, 3])
+def test_random_numerics_every_protocol(mode, world):
+    env, want = _NUMERICS_ENV[mode]
+    res = _gpu_launch(W.random_numerics, world, args=("cuda", mode), env=env, timeout_s=120)
+    for r in res:
+        bad = {k: v for k, v in r.items() if not v[0]}
+        assert not bad, bad
+        engines = {v[1] for k, v in r.items() if k.startswith("all_reduce/")}
+        if mode == "twoshot":
+            assert engines == {"ipc_2shot"}, engines
+        else:
+            assert all(e.startswith(want) for e in engines), engines

@@ -11,6 +11,9 @@ block_barrier, K4) must
   3. invalidate at system scope (``buffer_inv sc0 sc1``) after the poll, and wait
      for the invalidate, before any peer data is read.
 
+The kernels read their arguments from LDS (a gated zero-copy launch swaps peer buffers in
+there), typed as global pointers (dev_common.h ``gp``), so no access may be a flat one.
+
 Runs on the CPU box (llvm-objcopy + llvm-objdump from ROCm, no GPU)."""
 import os
 import re
@@ -88,6 +91,12 @@ def _ipc_kernels(funcs):
 def _check_barriers(name, body):
     wbl = [i for i, s in enumerate(body) if s == "buffer_wbl2 sc0 sc1"]
     inv = [i for i, s in enumerate(body) if s == "buffer_inv sc0 sc1"]
+    # the zero-copy gate (dev_common.h gate_wait): an acquire right after the 8-byte system-scope
+    # poll of the host-published slot's seq -- nothing is released before it (the host wrote it)
+    gate = [i for i in inv if any(body[j].startswith("global_load_dwordx2 ") and body[j].endswith("sc0 sc1")
+                                  for j in range(max(0, i - 3), i))]
+    assert gate, f"{name}: no system-scope acquire after the gate poll"
+    inv = [i for i in inv if i not in gate]
     assert wbl, f"{name}: no system-scope L2 write-back"
     assert len(wbl) == len(inv), f"{name}: {len(wbl)} releases vs {len(inv)} acquires"
     for w in wbl:
