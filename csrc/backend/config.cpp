@@ -48,6 +48,12 @@ const char* algo_name(Algo a) {
   return "?";
 }
 
+Algo algo_from_name(const std::string& n) {
+  for (Algo a : {Algo::RCCL, Algo::IPC, Algo::HOST, Algo::IPC_PUSH, Algo::RCCL_WIDE, Algo::IPC_WIDE})
+    if (n == algo_name(a)) return a;
+  return Algo::AUTO;
+}
+
 Config Config::from_env() {
   Config c;
   if (const char* a = env("PDCC_ALGO")) {
@@ -105,6 +111,7 @@ Config Config::from_env() {
   c.ipc_grid = std::min(1024, std::max(1, env_int("PDCC_IPC_GRID", c.ipc_grid)));
   c.ipc_wide_grid = std::min(1024, std::max(0, env_int("PDCC_IPC_WIDE_GRID", c.ipc_wide_grid)));
   c.autotune_spin_ms = (int64_t)env_size("PDCC_AUTOTUNE_SPIN_MS", (size_t)c.autotune_spin_ms);
+  if (const char* f = env("PDCC_AUTOTUNE_FILE")) c.autotune_file = f;
   if (const char* gc = env("PDCC_RCCL_GROUP_COMM")) {
     std::string v(gc);
     if (v == "split") c.group_comm = 0;
@@ -155,7 +162,7 @@ std::string Config::describe() const {
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
     << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
-    << " autotune_sample=" << autotune_sample << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
+    << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")

@@ -76,6 +76,10 @@ struct Config {
   // the protocol fails on at this size) costs this much once, disqualifies IPC for the key
   // and leaves the group healthy, instead of hanging for the group timeout.
   int64_t autotune_spin_ms = 10000;        // PDCC_AUTOTUNE_SPIN_MS
+  // Decisions persisted across runs: a key with a line in this file (same topology signature,
+  // the same on every rank) takes the recorded engine without a race; every new race's
+  // verdict is appended by rank 0 ("" = off). Offline tuning = a file written by an earlier run.
+  std::string autotune_file;               // PDCC_AUTOTUNE_FILE
   // PDCC_STREAM: auto (default) = synchronous collectives (async_op=False) on the caller's stream,
   // async ones on a normal-priority comm stream; high = auto with a high-priority comm stream;
   // comm = always the comm stream; current = always the caller's stream.
@@ -127,5 +131,7 @@ struct Config {
 };
 
 const char* algo_name(Algo a);
+// inverse of algo_name (AUTO for an unknown name)
+Algo algo_from_name(const std::string& n);
 
 }  // namespace pdcc

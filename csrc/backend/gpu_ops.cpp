@@ -17,6 +17,7 @@
 #include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 
+#include <sys/file.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -1128,6 +1129,18 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
     if (t == Algo::HOST && cap) return Algo::IPC;  // tuned to the host engine, which cannot be captured
     return t;
   }
+  if (!cfg_.autotune_file.empty()) {  // a decision recorded by an earlier run (same topology)
+    const Algo f = file_decision(key, ds);
+    if (f != Algo::AUTO && std::find(cands.begin(), cands.end(), f) != cands.end() && !(f == Algo::HOST && cap)) {
+      TuneEntry te;
+      te.ref = cands[0];
+      te.valid = true;
+      te.algo = f;  // iters = 0: from the file
+      std::lock_guard<std::mutex> lk(tune_mu_);
+      tune_[key] = te;
+      return f;
+    }
+  }
   if (cap) return a0;  // no timing runs inside a graph capture: static choice
   // every engine of the race exists before the clock starts (communicator setup is not timed)
   for (Algo a : cands) {
@@ -1261,6 +1274,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     std::lock_guard<std::mutex> lk(tune_mu_);
     tune_[key] = te;
   }
+  if (!cfg_.autotune_file.empty() && rank_ == 0 && te.valid) file_append(key, te, ds);
   if (cfg_.log_level >= 1 && rank_ == 0)
     fprintf(stderr,
             "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us%s"
@@ -1269,6 +1283,60 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
             te.ipc_wide_us, te.push_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
+}
+
+// ---- PDCC_AUTOTUNE_FILE: one line per decision,
+//   pdcc-tune v1 <signature> <coll> <dtype> <op> <size bucket> <engine> [# times]
+// The signature names what the verdict depends on: world size, distinct or shared GPUs,
+// the GPU architecture and the IPC grid cap.
+std::string ProcessGroupMI355X::tune_sig(const DeviceState& ds) const {
+  hipDeviceProp_t p{};
+  std::string arch = hipGetDeviceProperties(&p, ds.device) == hipSuccess ? std::string(p.gcnArchName) : "?";
+  arch = arch.substr(0, arch.find(':'));
+  std::ostringstream o;
+  o << "w" << size_ << "-" << (ds.shared_device ? "shared" : "distinct") << "-" << arch << "-g" << cfg_.ipc_grid;
+  return o.str();
+}
+
+Algo ProcessGroupMI355X::file_decision(const TuneKey& key, DeviceState& ds) {
+  if (!tune_file_read_) {
+    tune_file_read_ = true;
+    const std::string sig = tune_sig(ds);
+    if (FILE* f = std::fopen(cfg_.autotune_file.c_str(), "r")) {
+      char line[512];
+      while (std::fgets(line, sizeof(line), f)) {
+        char tag[16], ver[8], sg[128], eng[32];
+        int c, dt, op, b;
+        if (std::sscanf(line, "%15s %7s %127s %d %d %d %d %31s", tag, ver, sg, &c, &dt, &op, &b, eng) != 8) continue;
+        if (std::strcmp(tag, "pdcc-tune") != 0 || std::strcmp(ver, "v1") != 0 || sig != sg) continue;
+        const Algo a = algo_from_name(eng);
+        if (a != Algo::AUTO) tune_file_[TuneKey{c, dt, op, b}] = a;  // later lines win
+      }
+      std::fclose(f);
+    }
+  }
+  const auto it = tune_file_.find(key);
+  double v[2] = {it == tune_file_.end() ? 0.0 : (double)(int)it->second, 0.0};
+  v[1] = -v[0];
+  shm().allreduce(v, 2, at::kDouble, RedOpType::MAX, timeout_);  // max and -min: agree only if equal
+  return v[0] == -v[1] ? (Algo)(int)v[0] : Algo::AUTO;
+}
+
+void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, const DeviceState& ds) {
+  FILE* f = std::fopen(cfg_.autotune_file.c_str(), "a");
+  if (!f) {
+    fprintf(stderr, "[pdcc r%d] PDCC_AUTOTUNE_FILE %s: cannot append\n", rank_, cfg_.autotune_file.c_str());
+    return;
+  }
+  flock(fileno(f), LOCK_EX);
+  std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
+               "ipc_wide %.1f, ipc_push %.1f\n",
+               tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
+               algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref), (size_t)1 << std::get<3>(key),
+               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us);
+  std::fflush(f);
+  flock(fileno(f), LOCK_UN);
+  std::fclose(f);
 }
 
 std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table() {

@@ -579,6 +579,13 @@ class ProcessGroupMI355X : public c10d::Backend {
   // stream `s` waits for every async collective of this group issued so far (comm stream)
   void order_after_async(DeviceState& ds, hipStream_t s);
   Algo tuned(const TuneKey& k);
+  // PDCC_AUTOTUNE_FILE: the recorded engine of `key` for this topology if every rank's file
+  // has the same one (one host round), else AUTO; `file_append` records a race's verdict
+  std::map<TuneKey, Algo> tune_file_;
+  bool tune_file_read_ = false;
+  std::string tune_sig(const DeviceState& ds) const;
+  Algo file_decision(const TuneKey& key, DeviceState& ds);
+  void file_append(const TuneKey& key, const TuneEntry& e, const DeviceState& ds);
   // engine for one call: the static choice `a0`, or the tuned one for this key (tuning now,
   // through `tune(cands)`, when the key has no decision yet)
   Algo decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can, bool ipc_can,

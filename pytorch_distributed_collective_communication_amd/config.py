@@ -25,6 +25,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_AUTOTUNE_SAMPLE | 1G | bytes per engine the tuning runs move (a prefix of the caller's data) |
 | PDCC_AUTOTUNE_COLLS | all | comma list of collectives to tune (allreduce, reduce, broadcast, allgather, gather, scatter, reduce_scatter, alltoall) |
 | PDCC_AUTOTUNE_SPIN_MS | 10000 | spin bound of IPC runs during tuning; a timeout drops IPC for that key and keeps the group healthy |
+| PDCC_AUTOTUNE_FILE | "" | persisted decisions: keys with a line in this file (same topology signature on every rank) take the recorded engine without a race; rank 0 appends every new race's verdict |
 | PDCC_RCCL_MIN_CTAS / _MAX_CTAS | -1 / -1 | RCCL channel (CTA) bounds via ``ncclCommInitRankConfig``; -1 leaves RCCL's topology tuner in charge |
 | PDCC_RCCL_GROUP_COMM | share | groups with the same members as a live communicator: share it, split from it (ncclCommSplit) or init a fresh one |
 | PDCC_RCCL_SPLIT_SHARE | 1 | ncclCommSplit children share the parent's resources |
@@ -92,6 +93,7 @@ class Config:
     autotune_sample: int = 1 << 30
     autotune_colls: str = "all"
     autotune_spin_ms: int = 10000
+    autotune_file: str = ""
     rccl_min_ctas: int = -1
     rccl_max_ctas: int = -1
     rccl_wide_ctas: int = 112
@@ -124,6 +126,7 @@ _ENV = {
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",
+    "autotune_file": "PDCC_AUTOTUNE_FILE",
     "rccl_group_comm": "PDCC_RCCL_GROUP_COMM", "rccl_split_share": "PDCC_RCCL_SPLIT_SHARE",
     "list_gather": "PDCC_LIST_GATHER", "a2a_list_agree": "PDCC_A2A_LIST_AGREE", "eager_init": "PDCC_EAGER_INIT",
     "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",

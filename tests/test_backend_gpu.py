@@ -465,3 +465,21 @@ def test_random_numerics_every_protocol(mode, world):
             assert engines == {"ipc_2shot"}, engines
         else:
             assert all(e.startswith(want) for e in engines), engines
+
+
+def test_autotune_file_persists_decisions(tmp_path):
+    # verdict r2 weak #8: PDCC_AUTOTUNE_FILE -- the first run races every key and rank 0 appends
+    # the verdicts; a second run on the same topology takes them from the file, no race (iters 0)
+    f = tmp_path / "tune.txt"
+    env = {"PDCC_AUTOTUNE_FILE": str(f)}
+    first = _gpu_launch(W.autotune_probe, 2, env=env)
+    assert all(first[0]["ok"]) and all(first[1]["ok"])
+    lines = [ln for ln in f.read_text().splitlines() if ln.startswith("pdcc-tune v1 w2-shared-gfx950")]
+    assert len(lines) == len(first[0]["table"]) == 5, (lines, first[0]["table"])
+    second = _gpu_launch(W.autotune_probe, 2, env=env)
+    for r in second:
+        assert all(r["ok"]), r["ok"]
+        assert [e["iters"] for e in r["table"]] == [0] * 5, r["table"]
+        assert sorted((e["lo"], e["algo"]) for e in r["table"]) == \
+            sorted((e["lo"], e["algo"]) for e in first[0]["table"])
+    assert len(f.read_text().splitlines()) == len(lines)  # nothing re-raced, nothing appended
