@@ -46,8 +46,9 @@ pdcc::kern::RedOp kop(const std::string& s) {
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std::string& op, bool lds,
-                 int max_blocks, bool nt) {
+// mode: OR of kern::K1Mode bits (LDS-DMA engine, non-temporal stores, streaming kernel, non-temporal loads)
+void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std::string& op, int mode,
+                 int max_blocks) {
   TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= pdcc::kern::kMaxRanks, "reduce_nway: 1..8 sources");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && al16(out.data_ptr()), "reduce_nway: out must be a contiguous, "
               "16-byte aligned GPU tensor");
@@ -63,10 +64,8 @@ void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std
   TORCH_CHECK(pdcc::kern::supports(d, k), "reduce_nway: op '", op, "' unsupported for ", out.scalar_type());
   c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(out.device().index()).stream();
-  hipError_t e = lds ? pdcc::kern::reduce_nway(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
-                                               (int)srcs.size(), s, max_blocks, nt)
-                     : pdcc::kern::reduce_nway_regs(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
-                                                    (int)srcs.size(), s, max_blocks, nt);
+  hipError_t e = pdcc::kern::reduce_nway_mode(p.data(), (int)p.size(), out.data_ptr(), out.numel(), d, k,
+                                               (int)srcs.size(), s, max_blocks, mode);
   TORCH_CHECK(e == hipSuccess, "reduce_nway launch failed: ", hipGetErrorString(e));
 }
 
@@ -225,8 +224,9 @@ PYBIND11_MODULE(_C, m) {
       .def("log", &pdcc::IssueOrder::log);
 
   m.def("reduce_nway", &reduce_nway, py::arg("srcs"), py::arg("out"), py::arg("op") = "sum",
-        py::arg("lds") = true, py::arg("max_blocks") = 0, py::arg("nt") = false,
-        "K1: out = op(srcs...) on the current stream (nt: non-temporal destination stores)");
+        py::arg("mode") = 1, py::arg("max_blocks") = 0,
+        "K1: out = op(srcs...) on the current stream (mode: 1 LDS-DMA engine | 2 non-temporal stores | "
+        "4 streaming kernel | 8 non-temporal loads)");
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
         "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);

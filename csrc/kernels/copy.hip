@@ -267,6 +267,11 @@ hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t
                             int avg_div, hipStream_t stream, int max_blocks, bool nt) {
   return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, nt ? 2 : 0);
 }
+hipError_t reduce_nway_mode(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
+                            int avg_div, hipStream_t stream, int max_blocks, int mode) {
+  if (mode < 0 || mode > 15) return hipErrorInvalidValue;
+  return k1_dispatch(srcs, nsrc, out, count, t, op, avg_div, stream, max_blocks, mode);
+}
 
 // Default K2 grid from the launch's shape (scripts/k2_sweep.py on MI355X, profiles/README.md):
 // small lists are latency-bound and want one tile per workgroup; big streams want few,

@@ -55,6 +55,11 @@ hipError_t reduce_nway(const void* const* srcs, int nsrc, void* out, size_t coun
 hipError_t reduce_nway_regs(const void* const* srcs, int nsrc, void* out, size_t count, DType t,
                             RedOp op, int avg_div, hipStream_t stream, int max_blocks = 0, bool nt = false);
 
+// any K1 variant (`mode` = OR of K1Mode bits); the two calls above are LDS and REGS
+enum K1Mode : int { K1_LDS = 1, K1_NT = 2, K1_STREAM = 4, K1_NT_LOADS = 8 };
+hipError_t reduce_nway_mode(const void* const* srcs, int nsrc, void* out, size_t count, DType t, RedOp op,
+                            int avg_div, hipStream_t stream, int max_blocks, int mode);
+
 // ---------------------------------------------------------------- K2
 struct CopyDesc {
   const void* src;

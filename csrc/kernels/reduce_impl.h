@@ -88,6 +88,55 @@ __global__ void __launch_bounds__(256) k1_reduce_regs(Ptrs8 srcs, char* dst, siz
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
 
+// Streaming K1 (mode bit 2): no software pipeline and no loop -- each workgroup reduces one
+// slab of V 4 KiB tiles per source, every load issued before the first reduce, and the grid
+// covers the whole buffer (the shape of torch's elementwise kernels: the dispatcher keeps
+// every CU full of short workgroups, so the bytes in flight come from occupancy). NTL:
+// non-temporal source loads (read once), NT: non-temporal stores.
+template <int NSRC>
+struct StreamV {
+  static constexpr int value = NSRC <= 2 ? 4 : (NSRC <= 4 ? 2 : 1);
+};
+
+template <DType DT, RedOp OP, int NSRC, bool NT, bool NTL>
+__global__ void __launch_bounds__(256) k1_reduce_stream(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
+  constexpr int V = StreamV<NSRC>::value;
+  const size_t base = (size_t)blockIdx.x * (V * kTile) + threadIdx.x * 16;
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  if ((size_t)(blockIdx.x + 1) * (V * kTile) <= nbytes) {
+    uint4 v[V][NSRC];
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+#pragma unroll
+      for (int k = 0; k < NSRC; ++k) {
+        const char* p = srcs.p[k] + base + u * kTile;
+        if constexpr (NTL) {
+          const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+          v[u][k] = make_uint4(x[0], x[1], x[2], x[3]);
+        } else {
+          v[u][k] = *reinterpret_cast<const uint4*>(p);
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < V; ++u) store16<NT>(dst + base + u * kTile, reduce_vec<DT, OP, NSRC>(v[u], avg_div));
+    return;
+  }
+  // the last (partial) slab: bounded loads
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const size_t off = base + u * kTile;
+    if (off >= nbytes) return;
+    const uint32_t lim = (uint32_t)(nbytes - off < 16 ? nbytes - off : 16);
+    uint4 v[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k)
+      v[k] = lim == 16 ? *reinterpret_cast<const uint4*>(srcs.p[k] + off) : load_partial(srcs.p[k] + off, lim);
+    const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
+    if (lim == 16) *reinterpret_cast<uint4*>(dst + off) = r;
+    else store_partial(dst + off, r, lim);
+  }
+}
+
 // ------------------------------------------------------------- IPC reductions
 // Tile partitions (MUST be identical on every rank: a block only ever reads
 // tiles that the same-index block of each peer staged, which is what makes the
@@ -745,12 +794,28 @@ PDCC_DECL_DISPATCH(I32)
 PDCC_DECL_DISPATCH(I64)
 #undef PDCC_DECL_DISPATCH
 
-// `mode`: bit 0 = LDS-DMA engine (else registers), bit 1 = non-temporal stores
+// `mode` (kern::K1Mode): bit 0 = LDS-DMA engine (else registers), bit 1 = non-temporal stores,
+// bit 2 = the streaming kernel (one slab per workgroup, `grid` ignored), bit 3 = its loads
+// non-temporal too
 template <DType DT, RedOp OP, int NSRC>
 hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_div, hipStream_t s, int grid,
                      int mode) {
   Ptrs8 p{};
   for (int k = 0; k < NSRC; ++k) p.p[k] = (const char*)srcs[k];
+  if (mode & 4) {
+    const size_t slab = (size_t)StreamV<NSRC>::value * kTile;
+    const dim3 g((unsigned)((nbytes + slab - 1) / slab));
+    if (mode & 8)
+      hipLaunchKernelGGL((k1_reduce_stream<DT, OP, NSRC, true, true>), g, dim3(256), 0, s, p, (char*)out, nbytes,
+                         avg_div);
+    else if (mode & 2)
+      hipLaunchKernelGGL((k1_reduce_stream<DT, OP, NSRC, true, false>), g, dim3(256), 0, s, p, (char*)out, nbytes,
+                         avg_div);
+    else
+      hipLaunchKernelGGL((k1_reduce_stream<DT, OP, NSRC, false, false>), g, dim3(256), 0, s, p, (char*)out, nbytes,
+                         avg_div);
+    return hipGetLastError();
+  }
   static const int chunked = [] {
     const char* e = getenv("PDCC_K1_CHUNKED");
     return e && *e == '1' ? 1 : 0;

@@ -29,19 +29,25 @@ def _C():
     return _load_native()
 
 
+# K1 variants (csrc/kernels/kernel_api.h K1Mode): the LDS-DMA pipeline, the register pipeline,
+# the streaming kernel (one slab per workgroup, grid over the whole buffer); `_nt` =
+# non-temporal stores, `stream_ntl` = non-temporal loads and stores
+K1_IMPLS = {"lds": 1, "regs": 0, "lds_nt": 3, "regs_nt": 2, "stream": 4, "stream_nt": 6, "stream_ntl": 14}
+
+
 def reduce_nway(srcs: Sequence[torch.Tensor], out: torch.Tensor | None = None, op: str = "sum",
                 impl: str = "lds", max_blocks: int = 0) -> torch.Tensor:
     """K1 N-way element-wise reduction on the GPU (1 <= len(srcs) <= 8)."""
     if op not in _OPS:
         raise ValueError(f"op must be one of {_OPS}, got {op!r}")
-    if impl not in ("lds", "regs", "lds_nt", "regs_nt"):
-        raise ValueError(f"impl must be lds|regs|lds_nt|regs_nt, got {impl!r}")
+    if impl not in K1_IMPLS:
+        raise ValueError(f"impl must be one of {sorted(K1_IMPLS)}, got {impl!r}")
     srcs = list(srcs)
     if not srcs:
         raise ValueError("reduce_nway needs at least one source")
     if out is None:
         out = torch.empty_like(srcs[0], memory_format=torch.contiguous_format)
-    _C().reduce_nway(srcs, out, op, not impl.startswith("regs"), int(max_blocks), impl.endswith("_nt"))
+    _C().reduce_nway(srcs, out, op, K1_IMPLS[impl], int(max_blocks))
     return out
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """K1 tuning sweep (interleaved rounds in one process): grid size x engine for
-2/4/8-source fp32 reduces of 256 MiB per source (LDS-DMA / register engines, normal /
-non-temporal stores), plus torch baselines."""
+2/4/8-source fp32 reduces of 256 MiB per source (LDS-DMA / register pipelines with
+normal / non-temporal stores; the streaming kernel, grid over the whole buffer, with
+normal / non-temporal stores / non-temporal loads and stores), plus torch baselines."""
 import json
 import os
 import statistics
@@ -32,8 +33,8 @@ for nsrc in (2, 4, 8):
     dst = torch.empty_like(srcs[0])
     res = {}
     for _ in range(4):
-        for impl in ("lds", "regs", "lds_nt", "regs_nt"):
-            for g in (256, 512, 1024):
+        for impl in ("lds", "regs", "lds_nt", "regs_nt", "stream", "stream_nt", "stream_ntl"):
+            for g in ((256, 512) if not impl.startswith("stream") else (0,)):
                 t = timeit(lambda: ops.reduce_nway(srcs, out=dst, impl=impl, max_blocks=g))
                 res.setdefault(f"n{nsrc}_{impl}_g{g}", []).append((nsrc + 1) * n * 4 / t / 1e9)
         if nsrc == 2:

@@ -1,8 +1,8 @@
 """Numerics of the gfx950 kernels vs plain-PyTorch references (1 GPU).
 
 K1 reduce_nway: every op x dtype x source count, ragged sizes (tails that are
-not a multiple of the 16-B vector or the 4-KiB tile), both the LDS-DMA engine
-and the register-staged variant. Bitwise for MAX/MIN/integers; SUM/PROD/AVG in
+not a multiple of the 16-B vector or the 4-KiB tile), the LDS-DMA engine, the
+register-staged variant and the streaming kernel (normal and non-temporal). Bitwise for MAX/MIN/integers; SUM/PROD/AVG in
 low precision compared against an fp32-accumulated reference.
 K2 multi_copy / pack / unpack: ragged lists, mixed dtypes.
 """
@@ -35,7 +35,7 @@ def _rand(n, dt, dev, k):
     return torch.randint(lo, hi, (n,), generator=g, dtype=torch.int64).to(dt).to(dev)
 
 
-@pytest.mark.parametrize("impl", ["lds", "regs"])
+@pytest.mark.parametrize("impl", ["lds", "regs", "stream", "stream_ntl"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 @pytest.mark.parametrize("nsrc", [1, 2, 3, 5, 8])
 def test_reduce_nway_float(dt, nsrc, impl):
