@@ -389,7 +389,35 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
 }
 
 IpcComm::LaunchEvent::~LaunchEvent() {
-  if (ev) (void)hipEventDestroy(ev);
+  if (!ev) return;
+  if (pool) {
+    std::lock_guard<std::mutex> lk(pool->mu);
+    if (pool->free.size() < 256) {
+      pool->free.push_back(ev);
+      return;
+    }
+  }
+  (void)hipEventDestroy(ev);
+}
+
+IpcComm::EventPool::~EventPool() {
+  for (hipEvent_t e : free) (void)hipEventDestroy(e);
+}
+
+std::shared_ptr<IpcComm::LaunchEvent> IpcComm::new_launch_event(hipStream_t stream) {
+  auto le = std::make_shared<LaunchEvent>();
+  le->pool = ev_pool_;
+  {
+    std::lock_guard<std::mutex> lk(ev_pool_->mu);
+    if (!ev_pool_->free.empty()) {
+      le->ev = ev_pool_->free.back();
+      ev_pool_->free.pop_back();
+    }
+  }
+  DeviceScope ds(device_);
+  if (!le->ev) PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
+  PDCC_HIP(hipEventRecord(le->ev, stream));
+  return le;
 }
 
 void IpcComm::reap_closing(bool wait_all) {
@@ -491,11 +519,7 @@ void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipS
   // a captured launch reads exports pinned for the graph's lifetime (never evicted)
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
-  auto le = std::make_shared<LaunchEvent>();
-  DeviceScope ds(device_);
-  PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
-  PDCC_HIP(hipEventRecord(le->ev, stream));
-  zc_note_launch(le);
+  zc_note_launch(new_launch_event(stream));
 }
 
 void IpcComm::zc_note_launch(const std::shared_ptr<LaunchEvent>& le) {
@@ -529,10 +553,7 @@ void IpcComm::launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStrea
 }
 
 std::shared_ptr<IpcComm::LaunchEvent> IpcComm::gate_mark(uint64_t t, hipStream_t stream) {
-  auto le = std::make_shared<LaunchEvent>();
-  DeviceScope ds(device_);
-  PDCC_HIP(hipEventCreateWithFlags(&le->ev, hipEventDisableTiming));
-  PDCC_HIP(hipEventRecord(le->ev, stream));
+  auto le = new_launch_event(stream);
   gate_last_[t % kern::kGateSlots] = le;
   return le;
 }

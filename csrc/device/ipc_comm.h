@@ -117,6 +117,7 @@ class IpcComm {
   void launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStream_t stream);
   // after the launches of ticket `t`: their completion (slot reuse, mapping lifetime)
   struct LaunchEvent;
+  struct EventPool;
   std::shared_ptr<LaunchEvent> gate_mark(uint64_t t, hipStream_t stream);
   // exchange thread: the mappings just imported are read by the launches of `ev`
   void zc_note_launch(const std::shared_ptr<LaunchEvent>& ev);
@@ -159,14 +160,25 @@ class IpcComm {
   kern::GateSlot* gates_dev_ = nullptr;
   uint64_t gate_next_ = 0;
   std::vector<std::shared_ptr<LaunchEvent>> gate_last_;  // per slot: the launches that read it
+  std::shared_ptr<EventPool> ev_pool_ = std::make_shared<EventPool>();
   std::mutex zc_mu_;  // zc_exports_ (the caller exports, the exchange thread settles)
 
  public:
   // completion of one zero-copy launch (recorded on its stream right after it)
+  // Recycled completion events of zero-copy launches (one per call: creating a hipEvent on
+  // every call costs host time the enqueue path does not need to spend). A LaunchEvent hands
+  // its event back to the pool when the last reference to it goes (any thread).
+  struct EventPool {
+    std::mutex mu;
+    std::vector<hipEvent_t> free;
+    ~EventPool();
+  };
   struct LaunchEvent {
     hipEvent_t ev = nullptr;
+    std::shared_ptr<EventPool> pool;
     ~LaunchEvent();
   };
+  std::shared_ptr<LaunchEvent> new_launch_event(hipStream_t stream);  // recorded on `stream`
 
  private:
   struct ZcImport {
