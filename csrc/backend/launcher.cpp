@@ -106,7 +106,8 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
   std::shared_ptr<IpcComm> icp = ds.ipc;
   IpcLauncher& L = launcher(ds);
   std::lock_guard<std::mutex> lk(L.mu);
-  L.q.push_back([this, dsp = &ds, icp, mine, zbuf, t, ev] {
+  L.q.push_back([this, dsp = &ds, icp, mine, zbuf, t, ev, t_q = std::chrono::steady_clock::now()] {
+    const auto t_run = std::chrono::steady_clock::now();
     std::vector<char*> ptrs;
     bool ok = false;
     std::string err;
@@ -146,6 +147,10 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
       ++dsp->launcher->fallbacks;  // a rank could not export / map: this call runs staged
     }
     icp->gate_publish(t, ok, ptrs);
+    const auto t_end = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> lk3(dsp->launcher->mu);
+    dsp->launcher->wait_ns += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_run - t_q).count();
+    dsp->launcher->run_ns += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_end - t_run).count();
   });
   L.cv.notify_one();
 }

@@ -615,7 +615,7 @@ std::string ProcessGroupMI355X::describe() {
   o << "ProcessGroupMI355X(group=" << group_name_ << ", rank=" << rank_ << ", size=" << size_
     << ", same_host=" << same_host_ << ", timeout_ms=" << timeout_.count() << ", " << cfg_.describe();
   std::lock_guard<std::mutex> lk(init_mu_);
-  for (auto& kv : devs_)
+  for (auto& kv : devs_) {
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
       << ", zc_ok=" << kv.second->zc_ok << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
       << ", rccl=" << (kv.second->rccl != nullptr) << ", ipc=" << (kv.second->ipc != nullptr)
@@ -625,7 +625,15 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
-      << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0) << "}";
+      << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0);
+    if (kv.second->launcher) {
+      IpcLauncher& L = *kv.second->launcher;
+      std::lock_guard<std::mutex> lk2(L.mu);
+      if (L.jobs)
+        o << ", xchg_wait_us=" << (int)(L.wait_ns / 1e3 / L.jobs) << ", xchg_us=" << (int)(L.run_ns / 1e3 / L.jobs);
+    }
+    o << "}";
+  }
   o << ")";
   return o.str();
 }

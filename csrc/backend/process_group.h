@@ -215,6 +215,10 @@ struct IpcLauncher {
   bool busy = false, stop = false;
   std::thread thr;
   uint64_t jobs = 0, fallbacks = 0;
+  // time of the zero-copy jobs (describe(): xchg_wait_us / xchg_us, means): from the enqueue
+  // to the job's start (the thread's queue and wake-up), and the exchange itself (record
+  // all-gather with the peers' threads, mappings, gate publish)
+  double wait_ns = 0, run_ns = 0;
 };
 
 // whether `s` is being captured into a graph (launcher.cpp)

@@ -78,8 +78,21 @@ __device__ __forceinline__ uint4 ds_read16(uint32_t addr) {
   return v;
 }
 
+// NTL: non-temporal load (cache policy NT: streamed data read once)
+template <bool NTL = false>
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((gbl_cvoid_t*)g, (lds_void_t*)lds_wave_base, 16, 0, NTL ? 2 : 0);
+}
+
+template <bool NTL>
+__device__ __forceinline__ uint4 load16(const char* p) {
+  if constexpr (NTL) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+    return make_uint4(x[0], x[1], x[2], x[3]);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -225,7 +238,7 @@ __device__ __forceinline__ void store16(char* d, const uint4& r) {
   }
 }
 
-template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int NDST = 1, bool NT = false>
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map, int NDST = 1, bool NT = false, bool NTL = false>
 __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   static_assert((DEPTH - 1) * (NSRC + NDST) < 64, "pipeline too deep for vmcnt");
   static_assert(DEPTH >= 2 && DEPTH <= 8, "prologue wait counts are written out for DEPTH <= 8");
@@ -237,7 +250,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   auto issue = [&](size_t i, int stage) {
 #pragma unroll
     for (int s = 0; s < NSRC; ++s)
-      glds16(m.src(s, i) + lane_off, lds + (stage * NSRC + s) * kTile + wave * kWaveBytes);
+      glds16<NTL>(m.src(s, i) + lane_off, lds + (stage * NSRC + s) * kTile + wave * kWaveBytes);
   };
   auto consume = [&](size_t i, int stage) {
     const uint32_t a = lds_off(lds + stage * NSRC * kTile + lane_off);
@@ -309,7 +322,7 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
 
 // Register-staged engine (same Map contract): UNROLL tiles of NSRC vectors in
 // VGPRs per lane, no LDS. Kept for the A/B measurement against pipe_run.
-template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map, bool NT = false>
+template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map, bool NT = false, bool NTL = false>
 __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -322,7 +335,7 @@ __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
       for (int s = 0; s < NSRC; ++s)
-        v[u][s] = *reinterpret_cast<const uint4*>(m.src(s, i + u) + lane_off);
+        v[u][s] = load16<NTL>(m.src(s, i + u) + lane_off);
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint4 r = reduce_vec<DT, OP, NSRC>(v[u], avg_div);
@@ -335,7 +348,7 @@ __device__ __forceinline__ void pipe_run_regs(const Map& m, int avg_div) {
   for (; i < n; ++i) {
     uint4 v[NSRC];
 #pragma unroll
-    for (int s = 0; s < NSRC; ++s) v[s] = *reinterpret_cast<const uint4*>(m.src(s, i) + lane_off);
+    for (int s = 0; s < NSRC; ++s) v[s] = load16<NTL>(m.src(s, i) + lane_off);
     const uint4 r = reduce_vec<DT, OP, NSRC>(v, avg_div);
     char* d = m.dst(i);
     const size_t lim = m.valid(i);

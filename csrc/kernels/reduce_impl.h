@@ -18,6 +18,7 @@ struct Ptrs8 {
   const char* p[kern::kMaxRanks];
   int chunked;  // K1 tile->block map: 0 = strided (block b: b, b+G, ...), 1 = contiguous run per block
   int nt;       // K1 destination stores non-temporal (global_store ... nt)
+  int ntl;      // K1 source loads non-temporal
 };
 
 // LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU)
@@ -75,7 +76,8 @@ template <DType DT, RedOp OP, int NSRC, int D>
 __global__ void __launch_bounds__(256) k1_reduce_lds(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<NSRC, D>::kBytes];
   const StridedMap m = k1_map(srcs, dst, nbytes);
-  if (srcs.nt) pipe_run<DT, OP, NSRC, D, StridedMap, 1, true>(lds, m, avg_div);
+  if (srcs.ntl) pipe_run<DT, OP, NSRC, D, StridedMap, 1, true, true>(lds, m, avg_div);
+  else if (srcs.nt) pipe_run<DT, OP, NSRC, D, StridedMap, 1, true>(lds, m, avg_div);
   else pipe_run<DT, OP, NSRC, D>(lds, m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
@@ -83,7 +85,8 @@ __global__ void __launch_bounds__(256) k1_reduce_lds(Ptrs8 srcs, char* dst, size
 template <DType DT, RedOp OP, int NSRC>
 __global__ void __launch_bounds__(256) k1_reduce_regs(Ptrs8 srcs, char* dst, size_t nbytes, int avg_div) {
   const StridedMap m = k1_map(srcs, dst, nbytes);
-  if (srcs.nt) pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2), StridedMap, true>(m, avg_div);
+  if (srcs.ntl) pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2), StridedMap, true, true>(m, avg_div);
+  else if (srcs.nt) pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2), StridedMap, true>(m, avg_div);
   else pipe_run_regs<DT, OP, NSRC, (NSRC <= 2 ? 4 : 2)>(m, avg_div);
   if (blockIdx.x == gridDim.x - 1) reduce_tail<DT, OP, NSRC>(srcs.p, dst, nbytes, avg_div);
 }
@@ -822,6 +825,7 @@ hipError_t launch_k1(const void* const* srcs, void* out, size_t nbytes, int avg_
   }();
   p.chunked = chunked;
   p.nt = (mode & 2) ? 1 : 0;
+  p.ntl = (mode & 8) ? 1 : 0;  // (non-temporal loads come with non-temporal stores)
   const bool lds = (mode & 1) != 0;
   if (lds)
     hipLaunchKernelGGL((k1_reduce_lds<DT, OP, NSRC, K1Deep<NSRC>::value>), dim3(grid), dim3(256), 0, s, p, (char*)out,

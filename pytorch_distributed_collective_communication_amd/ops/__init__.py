@@ -31,8 +31,9 @@ def _C():
 
 # K1 variants (csrc/kernels/kernel_api.h K1Mode): the LDS-DMA pipeline, the register pipeline,
 # the streaming kernel (one slab per workgroup, grid over the whole buffer); `_nt` =
-# non-temporal stores, `stream_ntl` = non-temporal loads and stores
-K1_IMPLS = {"lds": 1, "regs": 0, "lds_nt": 3, "regs_nt": 2, "stream": 4, "stream_nt": 6, "stream_ntl": 14}
+# non-temporal stores, `_ntl` = non-temporal loads and stores
+K1_IMPLS = {"lds": 1, "regs": 0, "lds_nt": 3, "regs_nt": 2, "lds_ntl": 11, "regs_ntl": 10, "stream": 4,
+            "stream_nt": 6, "stream_ntl": 14}
 
 
 def reduce_nway(srcs: Sequence[torch.Tensor], out: torch.Tensor | None = None, op: str = "sum",

@@ -7,7 +7,9 @@ dist.all_reduce calls with the backend's stage profiler on (PDCC_HOST_PROF):
   per_call_us  -- wall time per call of the back-to-back loop incl. the GPU (max over ranks)
   stages_us    -- mean per call of each C++ stage (before_op, dev_state, choose, pre,
                   enqueue, work, record), and `c10d_python` = py_call - sum(stages)
-Cases: 4 B (LL kernel), 64 KiB (LL), 4 MiB async (zero-copy job on the IPC launcher).
+Cases: 4 B (LL kernel), 64 KiB (LL), 1 / 4 / 16 MiB sync and 4 MiB async (zero-copy: gated
+launch + exchange job on the IPC launcher thread; `xchg` = that thread's mean queue wait and
+exchange time per job).
 
     python scripts/host_path_bench.py [--calls 2000]
 """
@@ -30,7 +32,11 @@ def work(rank, size, calls):
     dev = torch.device("cuda", torch.cuda.current_device())
     b = be.native_backend(None, "cuda")
     out = {}
-    for name, nbytes, async_op in (("4B", 4, False), ("64KiB", 64 << 10, False), ("4MiB_async", 4 << 20, True)):
+    import re
+
+    cases = (("4B", 4, False), ("64KiB", 64 << 10, False), ("1MiB", 1 << 20, False), ("4MiB", 4 << 20, False),
+             ("4MiB_async", 4 << 20, True), ("16MiB", 16 << 20, False))
+    for name, nbytes, async_op in cases:
         x = torch.full((max(1, nbytes // 4),), 1.0, device=dev)
         for _ in range(50):
             w = dist.all_reduce(x, async_op=async_op)
@@ -56,6 +62,9 @@ def work(rank, size, calls):
         out[name] = {"algo": algo, "py_call_us": round(py, 2), "per_call_us": round(t.item() * 1e6, 2),
                      "stages_us": {s: round(v, 2) for s, v in stages.items()},
                      "c10d_python_us": round(py - sum(stages.values()), 2)}
+        m = re.search(r"launcher_jobs=(\d+).*?xchg_wait_us=(\d+), xchg_us=(\d+)", b.describe())
+        if m:  # zero-copy exchange thread, cumulative means (jobs so far)
+            out[name]["xchg"] = {"jobs": int(m.group(1)), "wait_us": int(m.group(2)), "run_us": int(m.group(3))}
         x.fill_(1.0)
         dist.all_reduce(x)
         out[name]["correct"] = bool(torch.all(x == size).item())

@@ -33,7 +33,7 @@ for nsrc in (2, 4, 8):
     dst = torch.empty_like(srcs[0])
     res = {}
     for _ in range(4):
-        for impl in ("lds", "regs", "lds_nt", "regs_nt", "stream", "stream_nt", "stream_ntl"):
+        for impl in ("lds", "lds_nt", "lds_ntl", "regs_nt", "regs_ntl", "stream_nt", "stream_ntl"):
             for g in ((256, 512) if not impl.startswith("stream") else (0,)):
                 t = timeit(lambda: ops.reduce_nway(srcs, out=dst, impl=impl, max_blocks=g))
                 res.setdefault(f"n{nsrc}_{impl}_g{g}", []).append((nsrc + 1) * n * 4 / t / 1e9)

@@ -2,7 +2,9 @@
 """Microbenchmark of the gfx950 kernels on one GPU (interleaved A/B rounds in
 one process, cdna_hip_programming.md §5.4 rule 24).
 
-K1 reduce_nway: LDS-DMA engine vs register-staged variant, nsrc in {2,4,8},
+K1 reduce_nway: LDS-DMA engine vs register-staged variant (normal stores), the LDS-DMA
+engine with non-temporal stores and the streaming kernel (non-temporal stores / loads and
+stores), nsrc in {2,4,8},
 fp32/bf16, 256 MiB per source (past the 256 MiB Infinity Cache for nsrc>=2).
 Effective bandwidth = (nsrc + 1) * bytes / time (every source read once, one write).
 K2 multi_copy: 64 tensors of 4 MiB, bandwidth = 2 * bytes / time.
@@ -40,9 +42,9 @@ def main():
         for nsrc in (2, 4, 8):
             srcs = [torch.rand(n, device=dev).to(dt) for _ in range(nsrc)]
             dst = torch.empty_like(srcs[0])
-            res = {"lds": [], "regs": []}
+            res = {k: [] for k in ("lds", "regs", "lds_nt", "stream_nt", "stream_ntl")}
             for _ in range(5):
-                for impl in ("lds", "regs"):
+                for impl in res:
                     t = timeit(lambda: ops.reduce_nway(srcs, out=dst, impl=impl))
                     res[impl].append((nsrc + 1) * per_src / t / 1e9)
             for impl in res:

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Small fixed workload for rocprofv3 --pmc runs (scripts/profile.sh pmc):
-K1 reduce_nway (LDS-DMA and register variants) on 2 and 8 fp32 sources of
+K1 reduce_nway (LDS-DMA, register, LDS-DMA with non-temporal stores, streaming with
+non-temporal stores / loads and stores) on 2 and 8 fp32 sources of
 64 MiB, K2 multi_copy of 16 x 4 MiB, and torch.add as the HBM reference.
 Each kernel runs 3 times, so per-dispatch counters (FETCH_SIZE, WRITE_SIZE,
 LDS bank conflicts) can be read straight off the counter CSV."""
@@ -19,7 +20,7 @@ def main():
     srcs = [torch.rand(n, device=dev) for _ in range(8)]
     out = torch.empty(n, device=dev)
     for nsrc in (2, 8):
-        for variant in ("lds", "regs"):
+        for variant in ("lds", "regs", "lds_nt", "stream_nt", "stream_ntl"):
             for _ in range(3):
                 ops.reduce_nway(srcs[:nsrc], out=out, op="sum", impl=variant)
     for _ in range(3):

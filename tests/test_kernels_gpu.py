@@ -35,7 +35,7 @@ def _rand(n, dt, dev, k):
     return torch.randint(lo, hi, (n,), generator=g, dtype=torch.int64).to(dt).to(dev)
 
 
-@pytest.mark.parametrize("impl", ["lds", "regs", "stream", "stream_ntl"])
+@pytest.mark.parametrize("impl", ["lds", "regs", "lds_ntl", "stream", "stream_ntl"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 @pytest.mark.parametrize("nsrc", [1, 2, 3, 5, 8])
 def test_reduce_nway_float(dt, nsrc, impl):
