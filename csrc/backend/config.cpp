@@ -146,6 +146,7 @@ Config Config::from_env() {
   c.shm_slot_bytes = env_size("PDCC_SHM_SLOT_BYTES", c.shm_slot_bytes);
   c.shm_chan_bytes = env_size("PDCC_SHM_CHAN_BYTES", c.shm_chan_bytes);
   c.shm_spin_us = (int)env_int("PDCC_SHM_SPIN_US", c.shm_spin_us);
+  c.xchg_spin_us = (int)env_int("PDCC_XCHG_SPIN_US", c.xchg_spin_us);
   c.debug = env_bool("PDCC_DEBUG", c.debug);
   c.log_level = env_int("PDCC_LOG_LEVEL", c.log_level);
   c.blocking_wait = env_bool("PDCC_BLOCKING_WAIT", c.blocking_wait);
@@ -167,7 +168,7 @@ std::string Config::describe() const {
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
     << " a2a_list_agree=" << a2a_list_agree
-    << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
+    << " xchg_spin_us=" << xchg_spin_us << " shm_slot=" << shm_slot_bytes << " shm_chan=" << shm_chan_bytes
     << " debug=" << debug << " log=" << log_level << " blocking_wait=" << blocking_wait
     << " watchdog_ms=" << watchdog_ms << " stream=" << (stream_mode == 0 ? "auto" : stream_mode == 1 ? "high" : stream_mode == 2 ? "comm" : "current");
   return o.str();

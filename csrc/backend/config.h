@@ -118,6 +118,8 @@ struct Config {
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES
   size_t shm_chan_bytes = 1u << 20;        // PDCC_SHM_CHAN_BYTES
   int shm_spin_us = 300;                   // PDCC_SHM_SPIN_US (busy-wait window before futex sleep)
+  // the zero-copy exchange thread spins this long after its last job before it sleeps
+  int xchg_spin_us = 500;                  // PDCC_XCHG_SPIN_US (0: sleep at once)
   // robustness / observability
   bool debug = false;                      // PDCC_DEBUG=1: cross-rank op fingerprint check
   int log_level = 0;                       // PDCC_LOG_LEVEL 0 quiet, 1 info, 2 every collective

@@ -41,14 +41,27 @@ void ProcessGroupMI355X::launcher_loop(DeviceState* dsp, IpcLauncher* lp) {
   (void)hipSetDevice(ds.device);
   // never a device-synchronising release on this thread (kernels wait for its exchanges)
   IpcComm::set_thread_defers_frees(true);
+  // Zero-copy calls come back to back, and every gated kernel waits for its job: a thread
+  // woken from a condition-variable sleep (measured 60-200 us per job on a busy box, r3
+  // host_path) would put that wake-up into every call. So the thread spins for
+  // PDCC_XCHG_SPIN_US after its last job before it sleeps.
+  const auto spin = std::chrono::microseconds(std::max(0, cfg_.xchg_spin_us));
+  uint64_t seen = 0;
   for (;;) {
     std::function<void()> job;
+    if (spin.count() > 0 && L.pushed.load(std::memory_order_acquire) == seen) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (L.pushed.load(std::memory_order_acquire) == seen && std::chrono::steady_clock::now() - t0 < spin)
+        __builtin_ia32_pause();
+    }
     {
       std::unique_lock<std::mutex> lk(L.mu);
       L.cv.wait(lk, [&] { return L.stop || !L.q.empty(); });
       if (L.q.empty()) return;  // stop, nothing left
       job = std::move(L.q.front());
       L.q.pop_front();
+      L.depth_sum += L.q.size();
+      ++seen;
       L.busy = true;
     }
     job();  // (never throws: a job publishes its gate slot whatever happens)
@@ -89,8 +102,11 @@ constexpr size_t kGateChunk = 256u << 20;
 void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen,
                                    size_t unit, size_t body, size_t per_call_max, hipStream_t s) {
   IpcComm& ic = ipc(ds);
+  hp_.lap(HostStage::ENQUEUE);
   const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, false);
+  hp_.lap(HostStage::ZC_EXPORT);
   const uint64_t t = ic.gate_reserve();
+  hp_.lap(HostStage::ZC_RESERVE);
   size_t chunk = std::min(per_call_max, kGateChunk) / unit * unit;
   if (chunk == 0) chunk = unit;
   for (size_t off = 0; off < body; off += chunk) {
@@ -100,15 +116,18 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
       if (call.in[k]) c.in[k] = static_cast<const char*>(call.in[k]) + off;
       if (call.out[k]) c.out[k] = static_cast<char*>(call.out[k]) + off;
     }
-    ic.launch_gated(c, t, off, s);
+    ic.launch_gated(c, t, off, mine, zbuf, s);
   }
+  hp_.lap(HostStage::ZC_LAUNCH);
   auto ev = ic.gate_mark(t, s);  // the launches that read the slot (and the mappings)
+  hp_.lap(HostStage::ZC_MARK);
   std::shared_ptr<IpcComm> icp = ds.ipc;
   IpcLauncher& L = launcher(ds);
   std::lock_guard<std::mutex> lk(L.mu);
   L.q.push_back([this, dsp = &ds, icp, mine, zbuf, t, ev, t_q = std::chrono::steady_clock::now()] {
     const auto t_run = std::chrono::steady_clock::now();
     std::vector<char*> ptrs;
+    double gather_ns = 0;
     bool ok = false;
     std::string err;
     try {
@@ -117,7 +136,10 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
       std::vector<IpcComm::ZcRec> all(size_);
       std::vector<void*> outs;
       for (auto& r : all) outs.push_back(&r);
+      const auto g0 = std::chrono::steady_clock::now();
       xc.allgather(&mine, outs, sizeof(mine), timeout_);
+      gather_ns = (double)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - g0)
+                      .count();
       bool all_ok = true, fresh = false;
       for (const auto& r : all) {
         all_ok = all_ok && r.ok;
@@ -151,8 +173,11 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
     std::lock_guard<std::mutex> lk3(dsp->launcher->mu);
     dsp->launcher->wait_ns += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_run - t_q).count();
     dsp->launcher->run_ns += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t_end - t_run).count();
+    dsp->launcher->gather_ns += gather_ns;
   });
+  L.pushed.fetch_add(1, std::memory_order_release);
   L.cv.notify_one();
+  hp_.lap(HostStage::ZC_JOB);
 }
 
 void ProcessGroupMI355X::stop_launchers() {

@@ -568,7 +568,9 @@ void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chr
 }
 
 std::vector<std::tuple<std::string, uint64_t, double>> ProcessGroupMI355X::host_profile() {
-  static const char* kNames[] = {"before_op", "dev_state", "choose", "pre", "enqueue", "work", "record"};
+  static const char* kNames[] = {"before_op", "dev_state", "choose", "pre", "enqueue", "work", "record",
+                                 "zc_export", "zc_reserve", "zc_launch", "zc_mark", "zc_job"};
+  static_assert(sizeof(kNames) / sizeof(kNames[0]) == (size_t)HostStage::N, "stage names");
   std::vector<std::tuple<std::string, uint64_t, double>> out;
   for (int i = 0; i < (int)HostStage::N; ++i) out.emplace_back(kNames[i], hp_.calls[i], hp_.ns[i] / 1e3);
   return out;
@@ -630,7 +632,9 @@ std::string ProcessGroupMI355X::describe() {
       IpcLauncher& L = *kv.second->launcher;
       std::lock_guard<std::mutex> lk2(L.mu);
       if (L.jobs)
-        o << ", xchg_wait_us=" << (int)(L.wait_ns / 1e3 / L.jobs) << ", xchg_us=" << (int)(L.run_ns / 1e3 / L.jobs);
+        o << ", xchg_wait_us=" << (int)(L.wait_ns / 1e3 / L.jobs) << ", xchg_us=" << (int)(L.run_ns / 1e3 / L.jobs)
+          << ", xchg_gather_us=" << (int)(L.gather_ns / 1e3 / L.jobs)
+          << ", xchg_depth_x10=" << (int)(10.0 * (double)L.depth_sum / (double)L.jobs);
     }
     o << "}";
   }

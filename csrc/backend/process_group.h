@@ -212,6 +212,7 @@ struct IpcLauncher {
   std::condition_variable cv;       // jobs / stop
   std::condition_variable idle_cv;  // queue drained and no job running
   std::deque<std::function<void()>> q;
+  std::atomic<uint64_t> pushed{0};  // jobs ever queued (polled lock-free while the thread spins)
   bool busy = false, stop = false;
   std::thread thr;
   uint64_t jobs = 0, fallbacks = 0;
@@ -219,6 +220,8 @@ struct IpcLauncher {
   // to the job's start (the thread's queue and wake-up), and the exchange itself (record
   // all-gather with the peers' threads, mappings, gate publish)
   double wait_ns = 0, run_ns = 0;
+  double gather_ns = 0;  // of run_ns: the record all-gather with the peers' threads
+  size_t depth_sum = 0;  // jobs still queued when a job starts (summed: mean queue depth)
 };
 
 // whether `s` is being captured into a graph (launcher.cpp)
@@ -260,6 +263,12 @@ enum class HostStage : int {
   ENQUEUE,     // the engine's enqueue: kernel launch / RCCL call / launcher job
   WORK,        // Work object, allocator stream records, watchdog registration
   RECORD,      // stats, last_algo, flight recorder
+  // inside ENQUEUE, a gated zero-copy call (launcher.cpp ipc_gated):
+  ZC_EXPORT,   // the caller's buffer record (allocation range, buffer id, cached export)
+  ZC_RESERVE,  // a gate slot (waits if the slot's launches of 64 calls ago still run)
+  ZC_LAUNCH,   // the gated kernel launch(es)
+  ZC_MARK,     // the completion event of the launches
+  ZC_JOB,      // the exchange job queued for the launcher thread
   N
 };
 struct HostProf {

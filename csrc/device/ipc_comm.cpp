@@ -115,6 +115,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
+  if (const char* zx = std::getenv("PDCC_IPC_ZX")) zx_on_ = std::atoi(zx) != 0;
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
@@ -133,6 +134,10 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     std::memset(gates_host_, 0, kern::kGateSlots * sizeof(kern::GateSlot));
     PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&gates_dev_), gates_host_, 0));
     gate_last_.assign(kern::kGateSlots, nullptr);
+    PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&ztab_host_), sizeof(kern::ZcTable),
+                           hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(ztab_host_, 0, sizeof(kern::ZcTable));
+    PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&ztab_dev_), ztab_host_, 0));
     if (const char* tr = std::getenv("PDCC_IPC_TRACE")) {
       const long n = std::atol(tr);
       if (n > 0) {
@@ -190,6 +195,7 @@ IpcComm::~IpcComm() {
     if (err_host_) hipHostFree(err_host_);
     gate_last_.clear();
     if (gates_host_) hipHostFree(gates_host_);
+    if (ztab_host_) hipHostFree(ztab_host_);
     if (trace_host_) hipHostFree(trace_host_);
   } catch (...) {
   }
@@ -429,11 +435,15 @@ void IpcComm::reap_closing(bool wait_all) {
     size_t keep = 0;
     for (size_t i = 0; i < zc_closing_.size(); ++i) {
       Closing& c = zc_closing_[i];
-      bool fin = !c.last || !c.last->ev;
-      if (!fin) {
-        const hipError_t e = wait_all ? hipEventSynchronize(c.last->ev) : hipEventQuery(c.last->ev);
-        fin = e != hipErrorNotReady;
+      bool fin = true;
+      for (const auto& le : c.last) {
+        if (!le || !le->ev) continue;
+        const hipError_t e = wait_all ? hipEventSynchronize(le->ev) : hipEventQuery(le->ev);
         (void)hipGetLastError();
+        if (e == hipErrorNotReady) {
+          fin = false;
+          break;
+        }
       }
       if (fin) done.push_back(std::move(c));
       else zc_closing_[keep++] = std::move(c);
@@ -457,9 +467,12 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
     auto& peer = zc_imports_[r];
     auto it = std::find_if(peer.begin(), peer.end(), [&](const ZcImport& im) { return im.id == all[r].evict; });
     if (it == peer.end()) continue;
+    tab_drop(r, it->tab);  // no kernel launched from now on finds it
     {
+      auto last = latest_gated();  // ... and the ones launched so far may still read through it
+      last.push_back(it->last);
       std::lock_guard<std::mutex> lk(closing_mu_);
-      zc_closing_.push_back({it->map, it->last});
+      zc_closing_.push_back({it->map, std::move(last)});
     }
     peer.erase(it);
   }
@@ -488,7 +501,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
         ok = false;
         continue;
       }
-      peer.push_back({all[r].id, m, nullptr});
+      peer.push_back({all[r].id, m, nullptr, tab_insert(r, all[r].id, m)});
       it = peer.end() - 1;
     }
     zc_cur_ids_[r] = all[r].id;
@@ -543,11 +556,41 @@ uint64_t IpcComm::gate_reserve() {
   return t;
 }
 
-void IpcComm::launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStream_t stream) {
+int IpcComm::tab_insert(int peer, uint64_t id, void* map) {
+  if (!ztab_host_ || peer < 0 || peer >= kern::kMaxRanks) return -1;
+  for (int j = 0; j < kern::kZcTab; ++j) {
+    if (__atomic_load_n(&ztab_host_->id[peer][j], __ATOMIC_ACQUIRE) != 0) continue;
+    __atomic_store_n(&ztab_host_->base[peer][j], reinterpret_cast<uint64_t>(map), __ATOMIC_RELAXED);
+    __atomic_store_n(&ztab_host_->id[peer][j], id, __ATOMIC_RELEASE);  // last: the kernels match on it
+    return j;
+  }
+  return -1;  // full: calls reading this buffer take the host gate
+}
+
+void IpcComm::tab_drop(int peer, int slot) {
+  if (!ztab_host_ || slot < 0) return;
+  __atomic_store_n(&ztab_host_->id[peer][slot], 0ull, __ATOMIC_RELEASE);
+  __atomic_store_n(&ztab_host_->base[peer][slot], 0ull, __ATOMIC_RELEASE);  // (kernels recheck id after base)
+}
+
+std::vector<std::shared_ptr<IpcComm::LaunchEvent>> IpcComm::latest_gated() {
+  std::lock_guard<std::mutex> lk(latest_mu_);
+  std::vector<std::shared_ptr<LaunchEvent>> v;
+  for (const auto& kv : latest_gated_) v.push_back(kv.second);
+  return v;
+}
+
+void IpcComm::launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, const ZcRec& mine, const void* self,
+                           hipStream_t stream) {
   call.zc = 0;
   call.gate = gates_dev_ + (t % kern::kGateSlots);
   call.gate_seq = t;
   call.zoff = zoff;
+  call.zx_tag = ++zx_tag_;  // gated launches run one after another (a group's collectives never overlap)
+  call.zx_id = !mine.ok ? kern::kZxNoExport : mine.id;
+  call.zx_off = mine.off;
+  call.zx_self = static_cast<char*>(const_cast<void*>(self));
+  call.ztab = zx_on_ ? ztab_dev_ : nullptr;
   prepare_staging(call, stream);  // (sized for either protocol, see ipc_staging_bytes)
   launch_view(view(peer_staging_), call, stream);
 }
@@ -555,6 +598,12 @@ void IpcComm::launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStrea
 std::shared_ptr<IpcComm::LaunchEvent> IpcComm::gate_mark(uint64_t t, hipStream_t stream) {
   auto le = new_launch_event(stream);
   gate_last_[t % kern::kGateSlots] = le;
+  {
+    std::lock_guard<std::mutex> lk(latest_mu_);
+    auto it = std::find_if(latest_gated_.begin(), latest_gated_.end(), [&](const auto& kv) { return kv.first == stream; });
+    if (it == latest_gated_.end()) latest_gated_.emplace_back(stream, le);
+    else it->second = le;
+  }
   return le;
 }
 

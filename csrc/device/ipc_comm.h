@@ -114,7 +114,10 @@ class IpcComm {
   // One launch of `call` (the staged view; whole units), gated on ticket `t`; `zoff` = its
   // byte offset inside every rank's buffer. Staging grows here (caller's thread) so the
   // staged fallback fits.
-  void launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, hipStream_t stream);
+  // `mine` / `self`: this rank's record and buffer for the device-side exchange (the kernel
+  // resolves the peers' buffers itself when every rank has them mapped already)
+  void launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, const ZcRec& mine, const void* self,
+                    hipStream_t stream);
   // after the launches of ticket `t`: their completion (slot reuse, mapping lifetime)
   struct LaunchEvent;
   struct EventPool;
@@ -185,13 +188,27 @@ class IpcComm {
     uint64_t id;
     void* map;  // hipIpcOpenMemHandle result (allocation base on this side)
     std::shared_ptr<LaunchEvent> last;  // the latest launch that read through this mapping
+    int tab = -1;  // its entry in the device-visible table (kern::ZcTable), -1 = none
   };
+  // Device-visible table of open mappings (pinned host memory; gated kernels look the peers'
+  // records up there, see kern::ZcTable). An entry is dropped (id = 0) before its mapping is
+  // queued for closing, and the close then also waits for the latest gated launch of every
+  // stream at that moment (any kernel that could have read the entry was launched by then).
+  bool zx_on_ = true;  // PDCC_IPC_ZX=0: gated kernels always wait for the host gate
+  uint64_t zx_tag_ = 0;  // gated launches so far (resolved slot = tag % kGateSlots)
+  kern::ZcTable* ztab_host_ = nullptr;
+  kern::ZcTable* ztab_dev_ = nullptr;
+  std::mutex latest_mu_;
+  std::vector<std::pair<hipStream_t, std::shared_ptr<LaunchEvent>>> latest_gated_;
+  int tab_insert(int peer, uint64_t id, void* map);
+  void tab_drop(int peer, int slot);
+  std::vector<std::shared_ptr<LaunchEvent>> latest_gated();
   // Evicted mappings are closed once the last launch that used them has finished (polled
   // at every exchange; the destructor waits): no device-wide synchronisation, so compute
   // streams and point-to-point pair streams are never drained by an eviction.
   struct Closing {
     void* map;
-    std::shared_ptr<LaunchEvent> last;
+    std::vector<std::shared_ptr<LaunchEvent>> last;  // every launch that may still read through it
   };
   mutable std::mutex closing_mu_;
   std::vector<Closing> zc_closing_;

@@ -78,14 +78,14 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
     case IpcColl::BROADCAST_2SHOT: {
       if (me != c.root) {  // phase 1: my owned tiles straight from the root's buffer into mine
         const OneSrcMap m{v.buf[c.root], v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       tr.mark(5);
       block_barrier(v, ep + 2u);
       tr.mark(6);
       if (me != c.root) {  // phase 2: the other owners' tiles (the root's own straight from the root)
         const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       break;
     }
@@ -93,19 +93,19 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
     case IpcColl::GATHER:
       if (c.coll == IpcColl::ALLGATHER || me == c.root) {
         const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(me + b), b, G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       tr.mark(5);
       break;
     case IpcColl::ALLTOALL: {
       const PeerTileMap<W> m{&v, &c, (size_t)me * c.zstride, c.bytes, (uint32_t)(me + b), b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       tr.mark(5);
       break;
     }
     case IpcColl::SCATTER: {  // my chunk straight out of the root's flat list
       const OneSrcMap m{v.buf[c.root] + (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       tr.mark(5);
       break;
     }
@@ -145,7 +145,7 @@ __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, ch
       tr.mark(4);
       if (me == c.root) return;
       const OneSrcMap m{v.buf[c.root] + poff, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
     case IpcColl::BROADCAST_2SHOT: {
@@ -155,13 +155,13 @@ __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, ch
       block_barrier(v, ph0);
       if (me != c.root) {  // phase 1: fetch my owned tiles from the root (one link each)
         const OneSrcMap m{v.buf[c.root] + poff, mine, cpad, me + W * b, W * G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       block_barrier(v, ph1);
       if (me == c.root) return;
       {  // phase 2: every owner's tiles, owners interleaved (all links at once)
         const OwnerRowMap<W> m{v.buf, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -174,7 +174,7 @@ __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, ch
       if (c.coll == IpcColl::GATHER && me != c.root) return;
       {
         const PeerTileMap<W> m{&v, &c, poff, c.bytes, (uint32_t)(me + b), b, G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -183,7 +183,7 @@ __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, ch
         for (int q = 0; q < W; ++q) stage_tiles((const char*)c.in[q], mine + q * cpad, c.bytes, b, G, nt);
       block_barrier(v, ph0);
       const OneSrcMap m{v.buf[c.root] + poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       return;
     }
     case IpcColl::ALLTOALL: {
@@ -191,7 +191,7 @@ __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, ch
       block_barrier(v, ph0);
       {
         const PeerTileMap<W> m{&v, &c, poff + me * cpad, c.bytes, (uint32_t)(me + b), b, G, nt};
-        pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -207,6 +207,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ DCall sc;
   PhaseTrace tr(v);
   stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_copy_body<W>(sv, sc, lds, tr);
   tr.finish(v);
 }
@@ -321,12 +322,13 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 }
 
 // block-pairwise flags, the per-block call counters, the LL control words and LL slots
-size_t ipc_signal_bytes() { return kLLOffset + 2 * (size_t)kMaxRanks * kLLSlotBytes; }
+size_t ipc_signal_bytes() { return kZxOffset + kZxBytes; }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
   if (c.gate) {  // either protocol may run: the larger need
     IpcCall z = c, st = c;
     z.gate = st.gate = nullptr;
+    z.ztab = st.ztab = nullptr;
     z.zc = 1;
     st.zc = 0;
     if (st.coll == IpcColl::ALLREDUCE_PUSH) st.coll = IpcColl::ALLREDUCE_2SHOT;

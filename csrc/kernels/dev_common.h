@@ -320,6 +320,18 @@ __device__ __forceinline__ void pipe_run(char* lds, const Map& m, int avg_div) {
   }
 }
 
+// The IPC kernels' pipelines. PDCC_IPC_NTL=1 makes their loads non-temporal (every source
+// tile is read once per call; K1 gains 8-11 % from it). Off: on one MI355X the A/B cost the
+// staged collectives 6-31 % at 4-64 MiB (profiles/r3/ipc_ntl_ab.md) -- their staging is
+// re-read in the next phase and otherwise stays in the 256 MiB Infinity Cache.
+#ifndef PDCC_IPC_NTL
+#define PDCC_IPC_NTL 0
+#endif
+template <DType DT, RedOp OP, int NSRC, int DEPTH, int NDST = 1, class Map>
+__device__ __forceinline__ void ipc_pipe(char* lds, const Map& m, int avg_div) {
+  pipe_run<DT, OP, NSRC, DEPTH, Map, NDST, false, PDCC_IPC_NTL != 0>(lds, m, avg_div);
+}
+
 // Register-staged engine (same Map contract): UNROLL tiles of NSRC vectors in
 // VGPRs per lane, no LDS. Kept for the A/B measurement against pipe_run.
 template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map, bool NT = false, bool NTL = false>
@@ -533,14 +545,178 @@ __device__ __forceinline__ bool gate_wait(const kern::IpcView& v, const kern::Ip
   }
 }
 
+// ---- device-side record exchange of a gated zero-copy launch (kern::ZcTable) ----------
+__device__ __forceinline__ uint64_t* zx_src_words(const kern::IpcView& v, int owner, int src) {
+  return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(v.flags[owner]) + kern::kZxOffset +
+                                     (size_t)src * kern::kZxSrcBytes);
+}
+__device__ __forceinline__ kern::GateSlot* zx_resolved(const kern::IpcView& v, uint64_t seq) {
+  return reinterpret_cast<kern::GateSlot*>(reinterpret_cast<char*>(v.flags[v.rank]) + kern::kZxResolvedOffset) +
+         (seq % kern::kGateSlots);
+}
+__device__ __forceinline__ void zx_put(uint64_t* p, uint32_t data, uint32_t tag) {
+  __hip_atomic_store(p, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wave 0 of block 0: push {id, off} to every rank, collect every rank's, look the peers' ids
+// up in this process's mapping table, vote, and publish the verdict in this call's resolved
+// slot (ok = 1 with the buffers, 2 = wait for the host gate, 0 = a peer never came: staged,
+// the error word is set). Returns nothing; every block reads the resolved slot.
+__device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::IpcCall& c) {
+  const int lane = threadIdx.x & 63, W = v.world, me = v.rank;
+  uint32_t* epw = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(v.flags[me]) + kern::kZxEpochOffset);
+  uint32_t ep = 0;
+  if (lane == 0) {  // only block 0 of this rank's gated kernels touches it, in stream order
+    ep = __hip_atomic_load(epw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_store(epw, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ep = __shfl(ep, 0);
+  if (ep == 0u) ep = 1u;  // (never tag 0: fresh signal memory is zero)
+  // round 1: my record into slot [me] of every rank (4 single-copy-atomic words)
+  if (lane < W) {
+    uint64_t* d = zx_src_words(v, lane, me);
+    zx_put(d + 0, (uint32_t)c.zx_id, ep);
+    zx_put(d + 1, (uint32_t)(c.zx_id >> 32), ep);
+    zx_put(d + 2, (uint32_t)c.zx_off, ep);
+    zx_put(d + 3, (uint32_t)(c.zx_off >> 32), ep);
+  }
+  uint64_t id = 0, off = 0;
+  bool got = lane >= W, alive = true;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t it = 1;; ++it) {
+    if (!got) {
+      const uint64_t* s = zx_src_words(v, me, lane);
+      uint64_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k] = __hip_atomic_load(s + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((uint32_t)(w[0] >> 32) == ep && (uint32_t)(w[1] >> 32) == ep && (uint32_t)(w[2] >> 32) == ep &&
+          (uint32_t)(w[3] >> 32) == ep) {
+        got = true;
+        id = (w[0] & 0xffffffffull) | (w[1] << 32);
+        off = (w[2] & 0xffffffffull) | (w[3] << 32);
+      }
+    }
+    if (__all(got)) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks ||
+        ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+      alive = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  // lookup: lanes 0-31 scan table row q = 2p, lanes 32-63 row 2p + 1 (loads issued together)
+  const kern::ZcTable* tab = c.ztab;
+  const int half = lane >> 5, j = lane & 31;
+  uint64_t cand[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int q = 2 * p + half;
+    cand[p] = (alive && q < W && q != me)
+                  ? __hip_atomic_load(&tab->id[q][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                  : 0ull;
+  }
+  uint64_t masks[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint64_t want = __shfl(id, 2 * p + half);  // row q's record id (lane q holds it)
+    masks[p] = __ballot(want != 0ull && want != kern::kZxNoExport && cand[p] == want);
+  }
+  uint64_t ptr = 0;
+  bool found = true;
+  if (lane < W) {
+    const uint64_t m = masks[lane >> 1] >> ((lane & 1) * 32) & 0xffffffffull;
+    if (lane == me) {
+      ptr = (uint64_t)(uintptr_t)static_cast<char*>(c.zx_self);
+    } else if (id == 0ull) {
+      ptr = 0;  // this peer shares nothing in this call
+    } else if (m != 0ull) {
+      const int jj = __builtin_ctzll(m);
+      const uint64_t base = __hip_atomic_load(&tab->base[lane][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      // the entry may have been dropped since the id load: recheck after reading base
+      found = base != 0ull && __hip_atomic_load(&tab->id[lane][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == id;
+      ptr = base + off;
+    } else {
+      found = false;
+    }
+  }
+  const bool mine_ok = alive && __all(found);
+  // round 2: the vote (word 4 of slot [me] at every rank)
+  bool all_ok = mine_ok;
+  if (alive) {
+    if (lane < W) zx_put(zx_src_words(v, lane, me) + 4, mine_ok ? 1u : 0u, ep);
+    bool have = lane >= W, yes = true;
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 1;; ++it) {
+      if (!have) {
+        const uint64_t w = __hip_atomic_load(zx_src_words(v, me, lane) + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(w >> 32) == ep) {
+          have = true;
+          yes = (uint32_t)w == 1u;
+        }
+      }
+      if (__all(have)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t1 > v.timeout_ticks ||
+          ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+        alive = false;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    all_ok = alive && __all(yes);
+  }
+  if (!alive && lane == 0) __hip_atomic_store(v.err, 0x800u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // publish for the kernel's blocks (uncached signal memory: relaxed words, seq last)
+  kern::GateSlot* res = zx_resolved(v, c.zx_tag);
+  if (lane < kern::kMaxRanks)
+    __hip_atomic_store(&res->ptr[lane], (all_ok && lane < W) ? ptr : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    __hip_atomic_store(&res->ok, !alive ? 0u : (all_ok ? 1u : 2u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) __hip_atomic_store(&res->seq, c.zx_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 of every block: the resolved slot of this call (block 0 publishes it). Returns the
+// verdict (0 / 1 / 2, see zx_resolve) and the buffers; false if the wait gave up.
+__device__ __forceinline__ bool zx_wait(const kern::IpcView& v, const kern::IpcCall& c, uint32_t& ok,
+                                        uint64_t (&ptrs)[kern::kMaxRanks]) {
+  kern::GateSlot* res = zx_resolved(v, c.zx_tag);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t it = 1;; ++it) {
+    if (__hip_atomic_load(&res->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == c.zx_tag) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+      __hip_atomic_store(v.err, 0x1000u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    if ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  ok = __hip_atomic_load(&res->ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int r = 0; r < kern::kMaxRanks; ++r) ptrs[r] = __hip_atomic_load(&res->ptr[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 __device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, DView& sv, DCall& sc) {
+  if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x < 64) zx_resolve(v, c);
   if (threadIdx.x == 0) {
     __builtin_memcpy(&sv, &v, sizeof(DView));  // same layout, pointers retyped global
     __builtin_memcpy(&sc, &c, sizeof(DCall));
     if (c.gate) {
       uint32_t ok = 0;
-      const bool live = gate_wait(v, c, ok);
-      if (live && ok) {
+      bool live = true, fast = false;
+      if (c.ztab) {
+        uint64_t ptrs[kern::kMaxRanks];
+        live = zx_wait(v, c, ok, ptrs);
+        if (live && ok == 1u) {
+          fast = true;
+          for (int r = 0; r < v.world; ++r) sv.buf[r] = reinterpret_cast<char*>((uintptr_t)ptrs[r]) + c.zoff;
+        }
+      }
+      if (live && !fast && (!c.ztab || ok == 2u)) live = gate_wait(v, c, ok);  // the host's verdict
+      if (fast) {
+        sc.zc = 1;
+      } else if (live && ok) {
         for (int r = 0; r < v.world; ++r)
           sv.buf[r] = reinterpret_cast<char*>((uintptr_t)__hip_atomic_load(&c.gate->ptr[r], __ATOMIC_RELAXED,
                                                                           __HIP_MEMORY_SCOPE_SYSTEM)) + c.zoff;

@@ -122,7 +122,7 @@ using IpcView = IpcViewT<RawPtr>;
 
 // Device-side phase trace of an IPC call (block 0, s_memrealtime ticks at 100 MHz):
 // [0] block 0's call number, [1] entry, [2] arrival barrier passed, [3] local data
-// staged, [4] data barrier passed, [5] first pull / reduce done, [6] second data
+// staged (a gated launch: its gate passed), [4] data barrier passed, [5] first pull / reduce done, [6] second data
 // barrier passed (2-shot), [7] exit. Record `seq % trace_cap`.
 constexpr int kTraceWords = 8;
 
@@ -189,6 +189,28 @@ struct GateSlot {
 };
 constexpr int kGateSlots = 64;
 
+// Device-side record exchange of a gated zero-copy launch (the steady state needs no host
+// thread). Block 0's wave 0 pushes this rank's record {allocation id, offset} to every peer
+// as flag-tagged 8-byte words (LL style, tag = a per-rank epoch of gated calls), looks the
+// peers' ids up in this process's table of open mappings (ZcTable, pinned host memory the
+// exchange thread maintains), votes (one more word per peer) and publishes the outcome
+// for the kernel's other blocks in a resolved slot (same layout as GateSlot, in the
+// uncached signal area): ok = 1 -> the peers' mapped buffers; ok = 2 -> some rank lacks a
+// mapping: wait for the host gate as before (the exchange thread opens it).
+constexpr int kZcTab = 32;  // mappings per peer the device can look up (>= PDCC_IPC_ZC_CACHE)
+struct ZcTable {
+  uint64_t id[kMaxRanks][kZcTab];    // allocation id (0 = free), written last
+  uint64_t base[kMaxRanks][kZcTab];  // the mapping of that allocation in this process
+};
+constexpr uint64_t kZxNoExport = ~0ull;  // record id of a rank whose buffer could not be exported
+// signal-area layout after the LL slots: per source rank 64 B (4 record words + 1 vote word),
+// the epoch word, then the resolved slots
+constexpr size_t kZxOffset = kLLOffset + 2 * (size_t)kMaxRanks * kLLSlotBytes;
+constexpr size_t kZxSrcBytes = 64;
+constexpr size_t kZxEpochOffset = kZxOffset + kMaxRanks * kZxSrcBytes;
+constexpr size_t kZxResolvedOffset = kZxOffset + 1024;
+constexpr size_t kZxBytes = 1024 + kGateSlots * sizeof(GateSlot);
+
 template <template <class> class P>
 struct IpcCallT {
   IpcColl coll;
@@ -210,6 +232,14 @@ struct IpcCallT {
   P<const GateSlot> gate;
   uint64_t gate_seq;
   size_t zoff;
+  // device-side exchange of a gated call (see ZcTable): this rank's record (allocation id,
+  // or 0 = nothing to share, kZxNoExport = not exportable; offset in the allocation), its own
+  // buffer, and the mapping table; ztab = null: wait for the host gate only
+  uint64_t zx_tag;  // this launch's number (one ticket may take several launches): its resolved slot
+  uint64_t zx_id;
+  uint64_t zx_off;
+  P<char> zx_self;
+  P<const ZcTable> ztab;
 };
 using IpcCall = IpcCallT<RawPtr>;
 

@@ -348,28 +348,28 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
     {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
     tr.mark(6);
     {  // phase 2: the other owners' reduced tiles
       const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
     }
   } else if (c.coll == IpcColl::ALLREDUCE_PUSH) {
     // every remote access is a write (xGMI writes are posted; reads wait a round trip)
     const size_t nrows = nt / W;
     {  // phase 1: my tiles to their owners' staging slots
       const PushMap<W> m{v.buf[me], v.stg, me, (uint32_t)b, b, G, nrows};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
     tr.mark(6);
     {  // phase 2: reduce my owned tiles, store the result into every rank's tensor
       const PushReduceMap<W> m{v.buf, v.stg[me], me, b, G, nrows};
-      pipe_run<DT, OP, W, D, PushReduceMap<W>, W>(lds, m, c.avg_div);
+      ipc_pipe<DT, OP, W, D, W>(lds, m, c.avg_div);
     }
     block_barrier(v, ep + 3u);  // departure with data: the peers' results are in my tensor
     return;
@@ -380,19 +380,19 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
     // reuse is guarded by the next call's arrival barrier).
     {
       const AllSrcMap<W> m{&v, 0, v.stg[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
     tr.mark(6);
     if (me == c.root) {
       const OwnerRowMap<W> m{v.stg, 0, v.buf[me], c.bytes, (uint32_t)(me + b), b, G, nt / W};
-      pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
     }
     return;
   } else if (c.coll == IpcColl::REDUCE_SCATTER) {
     const AllSrcMap<W> m{&v, (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
-    pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+    ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
     tr.mark(5);
   }
   block_barrier<false>(v, ep + 3u);  // departure
@@ -425,7 +425,7 @@ __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, 
       tr.mark(4);
       if (c.coll == IpcColl::REDUCE_1SHOT && me != c.root) return;
       const AllSrcMap<W> m{&v, poff, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
       tr.mark(5);
       return;
     }
@@ -439,7 +439,7 @@ __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, 
       // phase 1: reduce my owned tiles from every rank, in place into my staging
       {
         const AllSrcMap<W> m{&v, poff, mine, nt * kTile, me + W * b, W * G, nt};
-        pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+        ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
       }
       tr.mark(5);
       block_barrier(v, ph1);
@@ -448,7 +448,7 @@ __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, 
       // phase 2: pull every owner's reduced tiles, owners interleaved (all links at once)
       {
         const OwnerRowMap<W> m{v.buf, poff, (char*)c.out[0], c.bytes, (uint32_t)(me + b), b, G, (nt + W - 1) / W};
-        pipe_run<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        ipc_pipe<DT, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
       return;
     }
@@ -459,7 +459,7 @@ __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, 
       block_barrier(v, ph0);
       tr.mark(4);
       const AllSrcMap<W> m{&v, poff + me * cpad, (char*)c.out[0], c.bytes, b, G, nt};
-      pipe_run<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
       tr.mark(5);
       return;
     }
@@ -475,6 +475,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ DCall sc;
   PhaseTrace tr(v);
   stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);
   tr.finish(v);
 }

@@ -37,6 +37,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
 | PDCC_SHM_SPIN_US | 300 | host transport busy-wait window before a futex sleep (20 when ranks > CPUs) |
+| PDCC_XCHG_SPIN_US | 500 | the zero-copy exchange thread busy-waits this long for the next job before it sleeps (a wake-up per call would delay every gated kernel) |
 | PDCC_STREAM | auto | GPU stream policy: auto (sync ops on the caller's stream, async on a comm stream), high, comm, current |
 | PDCC_DEBUG | 0 | cross-rank fingerprint check before every collective |
 | PDCC_LOG_LEVEL | 0 | 1: group/device info, 2: every collective |
@@ -107,6 +108,7 @@ class Config:
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
     shm_spin_us: int = 300
+    xchg_spin_us: int = 500
     stream: str = "auto"
     debug: bool = False
     log_level: int = 0
@@ -132,7 +134,7 @@ _ENV = {
     "rccl_min_ctas": "PDCC_RCCL_MIN_CTAS", "rccl_max_ctas": "PDCC_RCCL_MAX_CTAS",
     "rccl_wide_ctas": "PDCC_RCCL_WIDE_CTAS", "rccl_wide_min": "PDCC_RCCL_WIDE_MIN",
     "shm_slot_bytes": "PDCC_SHM_SLOT_BYTES", "shm_chan_bytes": "PDCC_SHM_CHAN_BYTES",
-    "shm_spin_us": "PDCC_SHM_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
+    "shm_spin_us": "PDCC_SHM_SPIN_US", "xchg_spin_us": "PDCC_XCHG_SPIN_US", "stream": "PDCC_STREAM", "debug": "PDCC_DEBUG",
     "log_level": "PDCC_LOG_LEVEL", "blocking_wait": "PDCC_BLOCKING_WAIT", "roctx": "PDCC_ROCTX",
     "watchdog_ms": "PDCC_WATCHDOG_MS", "flight_recorder": "PDCC_FLIGHT_RECORDER", "fault": "PDCC_FAULT",
 }

@@ -62,6 +62,12 @@ for s in "$@"; do
     churntrace) step churntrace 400 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --hip-trace --stats --output-format csv \
         -d "$0/gpurun_out/prof_churn" -o churn_%pid% -- python3 "$0/scripts/zc_async_bench.py" --churn' "$(pwd)" ;;
     hostpath) step hostpath 300 python scripts/host_path_bench.py ;;
+    hostpathtr) step hostpathtr 300 python scripts/host_path_bench.py --trace ;;
+    hostpathinl) step hostpathinl 300 python scripts/host_path_bench.py --trace --env PDCC_IPC_ZC_ASYNC=0 ;;
+    hostpathspin0) step hostpathspin0 300 python scripts/host_path_bench.py --trace --env PDCC_XCHG_SPIN_US=0 ;;
+    cpuinfo) step cpuinfo 30 bash -c 'cat /sys/fs/cgroup/cpu.max 2>&1; cat /sys/fs/cgroup/cpuset.cpus.effective 2>&1; nproc; python3 -c "import os; print(len(os.sched_getaffinity(0)))"' ;;
+    hostprof) step hostprof 400 bash -c 'cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$0/gpurun_out/prof_host" -o hp_%pid% -- python3 "$0/scripts/host_path_bench.py" --calls 400' "$(pwd)" ;;
     tgdebug) step tgdebug 150 python scripts/zc_debug.py two_groups --world 2 --dump-s 40 --env PDCC_ALGO=ipc ;;
     k1sweep) step k1sweep 300 python scripts/k1_sweep.py ;;
     gpuA) step gpuA 1100 python -u -m pytest tests/test_backend_gpu.py -v --timeout 300 --timeout-method thread ;;

@@ -23,7 +23,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def work(rank, size, calls):
+def work(rank, size, calls, trace=False):
     import torch
     import torch.distributed as dist
 
@@ -32,6 +32,7 @@ def work(rank, size, calls):
     dev = torch.device("cuda", torch.cuda.current_device())
     b = be.native_backend(None, "cuda")
     out = {}
+    seen_seq = set()
     import re
 
     cases = (("4B", 4, False), ("64KiB", 64 << 10, False), ("1MiB", 1 << 20, False), ("4MiB", 4 << 20, False),
@@ -59,12 +60,28 @@ def work(rank, size, calls):
         py = statistics.median(host) * 1e6
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out_trace = None
         out[name] = {"algo": algo, "py_call_us": round(py, 2), "per_call_us": round(t.item() * 1e6, 2),
                      "stages_us": {s: round(v, 2) for s, v in stages.items()},
                      "c10d_python_us": round(py - sum(stages.values()), 2)}
-        m = re.search(r"launcher_jobs=(\d+).*?xchg_wait_us=(\d+), xchg_us=(\d+)", b.describe())
+        if trace:  # device phase trace of block 0 (PDCC_IPC_TRACE, 100 MHz ticks) of this case's IPC calls
+            recs = [r for r in b.ipc_trace() if r[0] not in seen_seq and r[1] and r[7]]
+            seen_seq.update(r[0] for r in recs)
+            if recs:
+                med = lambda xs: round(statistics.median(xs) / 100.0, 2)  # noqa: E731
+                gated = [r for r in recs if r[3] and r[2] and r[3] <= r[2]]  # [3] = gate passed (before arrival)
+                out_trace = {"calls": len(recs), "entry_to_arrival_us": med([r[2] - r[1] for r in recs if r[2]]),
+                             "gated_calls": len(gated),
+                             "gate_wait_us": med([r[3] - r[1] for r in gated]) if gated else None,
+                             "arrival_to_exit_us": med([r[7] - r[2] for r in recs if r[2]]),
+                             "kernel_us": med([r[7] - r[1] for r in recs])}
+        m = re.search(r"launcher_jobs=(\d+).*?xchg_wait_us=(\d+), xchg_us=(\d+), xchg_gather_us=(\d+), "
+                      r"xchg_depth_x10=(\d+)", b.describe())
         if m:  # zero-copy exchange thread, cumulative means (jobs so far)
-            out[name]["xchg"] = {"jobs": int(m.group(1)), "wait_us": int(m.group(2)), "run_us": int(m.group(3))}
+            out[name]["xchg"] = {"jobs": int(m.group(1)), "wait_us": int(m.group(2)), "run_us": int(m.group(3)),
+                                 "gather_us": int(m.group(4)), "queue_depth": int(m.group(5)) / 10}
+        if out_trace:
+            out[name]["device_trace"] = out_trace
         x.fill_(1.0)
         dist.all_reduce(x)
         out[name]["correct"] = bool(torch.all(x == size).item())
@@ -75,10 +92,16 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=2000)
     ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--trace", action="store_true", help="PDCC_IPC_TRACE: device phase times of block 0")
+    ap.add_argument("--env", nargs="*", default=[], help="extra KEY=VALUE for the ranks (e.g. PDCC_IPC_ZC_ASYNC=0)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
-    res = launch(work, a.world, args=(a.calls,), bind_device=True, timeout_s=60, env={"PDCC_ALGO": "ipc"},
+    env = {"PDCC_ALGO": "ipc"}
+    env.update(kv.split("=", 1) for kv in a.env)
+    if a.trace:
+        env["PDCC_IPC_TRACE"] = "65536"
+    res = launch(work, a.world, args=(a.calls, a.trace), bind_device=True, timeout_s=60, env=env,
                  join_timeout_s=300)
     for name, r in res[0].items():
         print(json.dumps({"world_on_one_gpu": a.world, "case": name, **r}), flush=True)
