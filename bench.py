@@ -320,15 +320,20 @@ def run_extras(world, rank, dev, native, x):
     from pytorch_distributed_collective_communication_amd import ops
 
     out = EXTRAS_PARTIAL  # filled in place, so a deadline still reports what finished
-    # K1 on this GPU: 2-source fp32 reduce of 256 MiB per source, LDS-DMA vs register staging
+    # K1 on this GPU: 2-source fp32 reduce of 256 MiB per source: LDS-DMA vs register staging,
+    # the non-temporal LDS-DMA default and the streaming kernel, and torch.add on the same data
     n = 64 << 20
     a = torch.rand(n, device=dev)
     b = torch.rand(n, device=dev)
     c = torch.empty_like(a)
-    for impl in ("lds", "regs"):
+    for impl in ("lds", "regs", "lds_ntl", "stream_ntl"):
         t = _time_op(lambda: ops.reduce_nway([a, b], out=c, impl=impl), 10) if world > 1 else _time_local(
             lambda: ops.reduce_nway([a, b], out=c, impl=impl), 10)
         out[f"k1_2src_f32_{impl}_GBps"] = round(3 * n * 4 / t / 1e9, 1)
+    t = _time_op(lambda: torch.add(a, b, out=c), 10) if world > 1 else _time_local(
+        lambda: torch.add(a, b, out=c), 10)
+    out["torch_add_2src_f32_GBps"] = round(3 * n * 4 / t / 1e9, 1)
+    ops.reduce_nway([a, b], out=c)
     ok = bool(torch.allclose(c, a + b))
     out["k1_correct"] = ok
     del a, b, c
