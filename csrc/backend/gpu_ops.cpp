@@ -649,6 +649,73 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
       fprintf(stderr, "[pdcc r%d] zero-copy IPC self-test failed (%s): group '%s' stages every IPC call\n", rank_,
               zok ? "on another rank" : zwhy.c_str(), group_name_.c_str());
   }
+  // Device-side record exchange of gated zero-copy launches (design.md §3): a gated all-reduce
+  // on a buffer every rank has mapped now must resolve on the device -- its host gate is not
+  // opened unless the kernel is still running after a grace period (then: staged fallback,
+  // and the device exchange stays off for the group)
+  if (ds.zc_ok && ds.ipc->zx_on()) {
+    bool xok = true;
+    std::string xwhy;
+    IpcComm& ic = *ds.ipc;
+    try {
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
+      const hipStream_t s = ds.stream.stream();
+      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
+      const int64_t row = (int64_t)size_ * (kern::kTileBytes / 4);
+      const at::Tensor base = at::arange(4 * row, opt).remainder(7);
+      at::Tensor x = base + (double)rank_;
+      // map x everywhere first (inline exchange through the store, like the zc self-test)
+      kern::IpcCall c{};
+      c.coll = kern::IpcColl::ALLREDUCE_2SHOT;
+      c.dtype = kern::DType::F32;
+      c.op = kern::RedOp::SUM;
+      c.avg_div = size_;
+      c.bytes = x.nbytes();
+      c.in[0] = x.data_ptr();
+      c.out[0] = x.data_ptr();
+      ipc_run(ds, c, x.data_ptr(), x.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s,
+              "pdcc/ipc_selftest/zx_map");
+      const IpcComm::ZcRec mine = ic.zc_export(x.data_ptr(), x.nbytes(), false);
+      const uint64_t t = ic.gate_reserve();
+      ic.launch_gated(c, t, 0, mine, x.data_ptr(), s);
+      auto ev = ic.gate_mark(t, s);
+      const uint64_t tag = ic.zx_last_tag();
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hipEventQuery(ev->ev) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(std::max<int64_t>(2000, spin_ms / 4)))
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      (void)hipGetLastError();
+      ic.gate_publish(t, false, {});  // (a kernel still waiting for the host gate runs staged now)
+      PDCC_HIP(hipStreamSynchronize(s));
+      const at::Tensor once = base * (double)size_ + size_ * (size_ - 1) / 2.0;  // after the mapping call
+      const bool data_ok = at::equal(x, once * (double)size_);
+      const uint32_t verdict = ic.zx_verdict(tag);
+      if (ic.error_word() != 0) {
+        xok = false;
+        xwhy = "the device exchange or a barrier timed out";
+        ic.clear_error();
+      } else if (verdict != 1u) {
+        xok = false;
+        xwhy = "the kernel did not resolve the buffers on the device (verdict " + std::to_string(verdict) + ")";
+      } else if (!data_ok) {
+        xok = false;
+        xwhy = "wrong data";
+      }
+    } catch (const std::exception& e) {
+      xok = false;
+      xwhy = e.what();
+    }
+    if (const char* f = std::getenv("PDCC_IPC_ZX_SELFTEST_FAIL"))  // test hook: this rank reports a failure
+      if (*f && std::atoi(f) == rank_) {
+        xok = false;
+        xwhy = "PDCC_IPC_ZX_SELFTEST_FAIL";
+      }
+    const bool zx = vote("pdcc/ipc_selftest/zx", xok);
+    ic.set_zx(zx);
+    if (!zx)
+      fprintf(stderr, "[pdcc r%d] device-side zero-copy exchange self-test failed (%s): group '%s' gates zero-copy "
+              "calls on the host\n", rank_, xok ? "on another rank" : xwhy.c_str(), group_name_.c_str());
+  }
   // LL all-reduce: payloads with a partial last line and the largest one, each twice
   // (both slot parities), bf16 and f32
   ds.ll_ok = false;

@@ -619,7 +619,10 @@ std::string ProcessGroupMI355X::describe() {
   std::lock_guard<std::mutex> lk(init_mu_);
   for (auto& kv : devs_) {
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
-      << ", zc_ok=" << kv.second->zc_ok << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
+      << ", zc_ok=" << kv.second->zc_ok << ", zx_ok=" << (kv.second->ipc ? kv.second->ipc->zx_on() : false)
+      << ", zx_fast=" << (kv.second->ipc ? kv.second->ipc->zx_fast() : 0)
+      << ", zx_host=" << (kv.second->ipc ? kv.second->ipc->zx_host() : 0)
+      << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
       << ", rccl=" << (kv.second->rccl != nullptr) << ", ipc=" << (kv.second->ipc != nullptr)
       << ", rccl_users=" << (kv.second->rccl ? kv.second->rccl->order().users() : 0)
       << ", rccl_issue_waits=" << (kv.second->rccl ? kv.second->rccl->order().waits() : 0)

@@ -553,6 +553,11 @@ uint64_t IpcComm::gate_reserve() {
     (void)hipGetLastError();
   }
   prev.reset();
+  kern::GateSlot* g = gates_host_ + (t % kern::kGateSlots);
+  const uint32_t v = __atomic_exchange_n(&g->verdict, 0u, __ATOMIC_ACQ_REL);  // ticket t - kGateSlots's launch
+  if (v == 0x101u) ++zx_fast_;
+  else if (v == 0x102u) ++zx_host_;
+  else if (v == 0x100u) ++zx_failed_;
   return t;
 }
 
@@ -571,6 +576,15 @@ void IpcComm::tab_drop(int peer, int slot) {
   if (!ztab_host_ || slot < 0) return;
   __atomic_store_n(&ztab_host_->id[peer][slot], 0ull, __ATOMIC_RELEASE);
   __atomic_store_n(&ztab_host_->base[peer][slot], 0ull, __ATOMIC_RELEASE);  // (kernels recheck id after base)
+}
+
+uint32_t IpcComm::zx_verdict(uint64_t tag) {
+  DeviceScope ds(device_);
+  kern::GateSlot r{};
+  const char* slot = reinterpret_cast<const char*>(my_flags_) + kern::kZxResolvedOffset +
+                     (tag % kern::kGateSlots) * sizeof(kern::GateSlot);
+  PDCC_HIP(hipMemcpy(&r, slot, sizeof(r), hipMemcpyDeviceToHost));
+  return r.seq == tag ? r.ok : 0xffffffffu;
 }
 
 std::vector<std::shared_ptr<IpcComm::LaunchEvent>> IpcComm::latest_gated() {

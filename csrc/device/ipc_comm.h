@@ -21,6 +21,7 @@
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -118,6 +119,17 @@ class IpcComm {
   // resolves the peers' buffers itself when every rank has them mapped already)
   void launch_gated(kern::IpcCall call, uint64_t t, size_t zoff, const ZcRec& mine, const void* self,
                     hipStream_t stream);
+  // device-side exchange (kern::ZcTable): on / off for this group (the self-test turns it
+  // off when it fails), the last gated launch's tag and, once it finished, its verdict
+  // (1 = resolved on the device, 2 = waited for the host gate, 0 = exchange gave up)
+  bool zx_on() const { return zx_on_; }
+  void set_zx(bool on) { zx_on_ = on; }
+  uint64_t zx_last_tag() const { return zx_tag_; }
+  // verdicts of the gated launches whose slots were reused so far (device / host gate / gave up)
+  uint64_t zx_fast() const { return zx_fast_; }
+  uint64_t zx_host() const { return zx_host_; }
+  uint64_t zx_failed() const { return zx_failed_; }
+  uint32_t zx_verdict(uint64_t tag);
   // after the launches of ticket `t`: their completion (slot reuse, mapping lifetime)
   struct LaunchEvent;
   struct EventPool;
@@ -196,6 +208,7 @@ class IpcComm {
   // stream at that moment (any kernel that could have read the entry was launched by then).
   bool zx_on_ = true;  // PDCC_IPC_ZX=0: gated kernels always wait for the host gate
   uint64_t zx_tag_ = 0;  // gated launches so far (resolved slot = tag % kGateSlots)
+  std::atomic<uint64_t> zx_fast_{0}, zx_host_{0}, zx_failed_{0};
   kern::ZcTable* ztab_host_ = nullptr;
   kern::ZcTable* ztab_dev_ = nullptr;
   std::mutex latest_mu_;

@@ -674,7 +674,12 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   }
   __builtin_amdgcn_wave_barrier();
-  if (lane == 0) __hip_atomic_store(&res->seq, c.zx_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) {
+    __hip_atomic_store(&res->seq, c.zx_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    // for the host's statistics (read when the gate slot is reused): a posted store, off the critical path
+    __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), 0x100u | (!alive ? 0u : (all_ok ? 1u : 2u)),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Thread 0 of every block: the resolved slot of this call (block 0 publishes it). Returns the

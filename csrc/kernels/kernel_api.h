@@ -184,7 +184,7 @@ inline bool is_ll(IpcColl c) {
 struct GateSlot {
   uint64_t seq;              // == IpcCall::gate_seq once `ok` and `ptr` are valid (written last)
   uint32_t ok;
-  uint32_t pad;
+  uint32_t verdict;          // written by the kernel: how its device-side exchange ended (see ZcTable)
   uint64_t ptr[kMaxRanks];   // rank r's buffer of the call, mapped into this process (own: local)
 };
 constexpr int kGateSlots = 64;

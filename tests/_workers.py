@@ -1483,3 +1483,30 @@ def random_numerics(rank, size, device="cuda", mode="ll"):
             out[f"reduce_scatter/{dtn}/SUM/{m}"] = [_close(o.cpu(), mine, "SUM", size, dtn), gb.last_algo()]
     dist.barrier()
     return out
+
+
+def zx_steady_probe(rank, size, device="cuda", calls=100, n=(4 << 20) // 4):
+    """Steady-state zero-copy: `calls` async all_reduces on one 4 MiB tensor. The buffer is
+    mapped once; from then on the gated kernels resolve the peers' buffers on the device
+    (zx_fast in describe() counts the launches that did, once their gate slots are reused)."""
+    import re
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    x = torch.empty(n, device=d)
+    ok = True
+    for i in range(calls):
+        x.fill_(float(rank + i))
+        dist.all_reduce(x, async_op=True).wait()
+        if i % 10 == 9:
+            ok = ok and bool(torch.all(x == sum(r + i for r in range(size))))
+    torch.cuda.current_stream().synchronize()
+    desc = b.describe()
+    m = re.search(r"zx_fast=(\d+), zx_host=(\d+)", desc)
+    return {"ok": ok, "algo": b.last_algo(), "fast": int(m.group(1)) if m else -1,
+            "host": int(m.group(2)) if m else -1, "desc": desc}

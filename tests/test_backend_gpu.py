@@ -431,13 +431,25 @@ def test_zero_copy_gated_launches_then_device_sync():
         assert all(ok.values()), ok
 
 
-@pytest.mark.parametrize("cache", ["4", "16"])
-def test_zero_copy_eviction_churn(cache):
+@pytest.mark.parametrize("cache,zx", [("4", "1"), ("16", "1"), ("4", "0")])
+def test_zero_copy_eviction_churn(cache, zx):
     # 40 distinct allocations through a cache of 4/16 exports: evicted mappings close after
-    # their last launch (deferred, no hipDeviceSynchronize), every result exact
-    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": cache}
+    # their last launch (deferred, no hipDeviceSynchronize), every result exact; with the
+    # device-side record exchange (zx=1: mapping-table entries dropped and re-filled under the
+    # running kernels) and with the host gate only (PDCC_IPC_ZX=0)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": cache, "PDCC_IPC_ZX": zx}
     for r in _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120):
         assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+        assert f"zx_ok={zx}" in r["desc"], r["desc"]
+
+
+def test_zero_copy_device_exchange_selftest_gate():
+    # the device-side exchange has its own self-test: one rank reporting a failure turns it off
+    # for the whole group (zx_ok=0), and zero-copy calls keep working through the host gate
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZX_SELFTEST_FAIL": "1"}
+    for r in _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120):
+        assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+        assert "zx_ok=0" in r["desc"] and "zc_ok=1" in r["desc"], r["desc"]
 
 
 # verdict r2 #6: random-data numerics of every IPC protocol through the collective API,
@@ -483,3 +495,11 @@ def test_autotune_file_persists_decisions(tmp_path):
         assert sorted((e["lo"], e["algo"]) for e in r["table"]) == \
             sorted((e["lo"], e["algo"]) for e in first[0]["table"])
     assert len(f.read_text().splitlines()) == len(lines)  # nothing re-raced, nothing appended
+
+
+def test_zero_copy_steady_state_resolves_on_the_device():
+    # one buffer, 100 async zero-copy all_reduces: after the first call mapped it, the kernels
+    # find every peer's buffer in the mapping table themselves (no host gate on the critical path)
+    for r in _gpu_launch(W.zx_steady_probe, 2, env={"PDCC_ALGO": "ipc"}, timeout_s=120):
+        assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+        assert r["fast"] >= 30 and r["host"] <= 2, (r["fast"], r["host"], r["desc"])
