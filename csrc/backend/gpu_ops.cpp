@@ -949,7 +949,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
     }
   }
   ok = ok && all_ok;
-  ic.zc_settle(ok);
+  ic.zc_settle(mine, ok);
   if (!ok) return 0;
   if (call.coll == kern::IpcColl::REDUCE_2SHOT || call.coll == kern::IpcColl::ALLREDUCE_PUSH) {
     // the rooted reduce stages its reduced tiles, the push all-reduce receives its owned

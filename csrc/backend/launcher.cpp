@@ -152,7 +152,7 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
         ok = f > 0.0;
       }
       ok = ok && all_ok;
-      icp->zc_settle(ok);
+      icp->zc_settle(mine, ok);
       if (ok) icp->zc_note_launch(ev);
     } catch (const std::exception& e) {
       err = e.what();

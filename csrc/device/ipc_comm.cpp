@@ -334,7 +334,6 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
 IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   std::lock_guard<std::mutex> zl(zc_mu_);
   ZcRec r{};
-  zc_pending_ = false;
   if (!p && len == 0) {  // this rank has nothing the peers read (a scatter's non-root)
     r.ok = 1;
     return r;
@@ -387,10 +386,6 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   r.off = off;
   r.len = len;
   r.handle = it->handle;
-  if (r.fresh) {
-    zc_pending_ = true;
-    zc_pending_id_ = id;
-  }
   return r;
 }
 
@@ -510,16 +505,16 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
   return ok;
 }
 
-void IpcComm::zc_settle(bool ok) {
+void IpcComm::zc_settle(const ZcRec& mine, bool ok) {
+  // (the record of the exchange being settled, not the latest export: with gated launches the
+  // caller may have exported later calls' buffers before this exchange ran)
+  if (!mine.ok || !mine.fresh || mine.id == 0) return;
   std::lock_guard<std::mutex> zl(zc_mu_);
-  if (!zc_pending_) return;
-  auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(),
-                         [&](const ZcExport& e) { return e.id == zc_pending_id_; });
+  auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(), [&](const ZcExport& e) { return e.id == mine.id; });
   if (it != zc_exports_.end()) {
     if (ok) it->confirmed = true;
-    else if (!it->pinned) zc_exports_.erase(it);  // announced fresh again next time
+    else if (!it->pinned && !it->confirmed) zc_exports_.erase(it);  // announced fresh again next time
   }
-  zc_pending_ = false;
 }
 
 void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream) {

@@ -81,7 +81,7 @@ class IpcComm {
   // One rank's buffer, exchanged over the host transport before the launch (the
   // caller drives the exchange; every rank runs the same steps):
   //   rec = zc_export(p, len)  ->  all-gather recs  ->  zc_import(all, ...)  ->
-  //   [fresh anywhere: agree on the import result]  ->  zc_settle(ok)  ->  launch_zc.
+  //   [fresh anywhere: agree on the import result]  ->  zc_settle(mine, ok)  ->  launch_zc.
   // `id` is the exporter's allocation id (HIP BUFFER_ID): an allocation freed and
   // re-made at the same address gets a new one, so nobody reads through a stale
   // mapping. Importers keep a mapping until its exporter evicts it (`evict`, LRU
@@ -104,7 +104,7 @@ class IpcComm {
   // (own = `mine`). False if a mapping failed on this rank.
   bool zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs);
   // group-wide outcome of this exchange: this rank's fresh export is confirmed or dropped
-  void zc_settle(bool ok);
+  void zc_settle(const ZcRec& mine, bool ok);
   // one zero-copy launch (call.zc is set here); bufs[r] = rank r's mapped buffer
   void launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipStream_t stream);
 
@@ -232,8 +232,6 @@ class IpcComm {
   std::vector<std::vector<ZcImport>> zc_imports_;  // per peer
   size_t zc_cache_ = 16;
   uint64_t zc_tick_ = 0;
-  bool zc_pending_ = false;  // an export was announced fresh in the exchange in progress ...
-  uint64_t zc_pending_id_ = 0;  // ... this one
 
   c10::intrusive_ptr<c10d::Store> store_;
   std::string key_;
