@@ -147,7 +147,8 @@ def run(rank: int, world: int, dev, deadline_s: float = 45.0, max_bytes: int = 6
     ipc_ok = "ipc_ok=1" in desc
     zc_ok = "zc_ok=1" in desc
     ll_ok = "ll_ok=1" in desc
-    info = {"world": world, "device": dev.type, "rccl_ok": rccl_ok, "ipc_ok": ipc_ok, "zc_ok": zc_ok, "ll_ok": ll_ok}
+    info = {"world": world, "device": dev.type, "rccl_ok": rccl_ok, "ipc_ok": ipc_ok, "zc_ok": zc_ok, "ll_ok": ll_ok,
+            "zx_ok": "zx_ok=1" in desc}  # zero-copy records exchanged on the device (design.md §3)
     if engines is None:
         if not on_gpu or world == 1:
             engines = ["auto"]
