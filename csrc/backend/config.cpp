@@ -44,12 +44,13 @@ const char* algo_name(Algo a) {
     case Algo::IPC_PUSH: return "ipc_push";
     case Algo::RCCL_WIDE: return "rccl_wide";
     case Algo::IPC_WIDE: return "ipc_wide";
+    case Algo::IPC_STAGED: return "ipc_staged";
   }
   return "?";
 }
 
 Algo algo_from_name(const std::string& n) {
-  for (Algo a : {Algo::RCCL, Algo::IPC, Algo::HOST, Algo::IPC_PUSH, Algo::RCCL_WIDE, Algo::IPC_WIDE})
+  for (Algo a : {Algo::RCCL, Algo::IPC, Algo::HOST, Algo::IPC_PUSH, Algo::RCCL_WIDE, Algo::IPC_WIDE, Algo::IPC_STAGED})
     if (n == algo_name(a)) return a;
   return Algo::AUTO;
 }
@@ -65,7 +66,8 @@ Config Config::from_env() {
     else if (s == "ipc_push") c.force_algo = Algo::IPC_PUSH;
     else if (s == "rccl_wide") c.force_algo = Algo::RCCL_WIDE;
     else if (s == "ipc_wide") c.force_algo = Algo::IPC_WIDE;
-    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|host, got " + s);
+    else if (s == "ipc_staged") c.force_algo = Algo::IPC_STAGED;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|host, got " + s);
   }
   c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
   c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);

@@ -14,8 +14,13 @@ namespace pdcc {
 // with at least rccl_wide_ctas channels, an autotuner candidate next to the default one.
 // IPC_WIDE: the pull all-reduce with ipc_wide_grid workgroups (more remote reads in flight
 // per xGMI link), an autotuner candidate next to IPC for bulk all_reduce keys.
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE };
-inline bool is_ipc(Algo a) { return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE; }
+// IPC_STAGED: the IPC protocols with zero copy off for the call (inputs copied into the
+// registered staging buffer): raced against IPC (zero copy) for keys from ipc_zc_min, so the
+// zero-copy / staging crossover is measured per node instead of fixed.
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE, IPC_STAGED };
+inline bool is_ipc(Algo a) {
+  return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE || a == Algo::IPC_STAGED;
+}
 inline bool is_rccl(Algo a) { return a == Algo::RCCL || a == Algo::RCCL_WIDE; }
 
 struct Config {

@@ -869,6 +869,7 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
       return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_WIDE && ipc_can)  // only all_reduce races the wide grid
       return c == Coll::ALLREDUCE ? Algo::IPC_WIDE : Algo::IPC;
+    if (cfg_.force_algo == Algo::IPC_STAGED && ipc_can) return Algo::IPC_STAGED;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
       if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
@@ -910,7 +911,7 @@ void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per
 // have not mapped yet (agreeing that every mapping worked).
 size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen,
                                          size_t unit, hipStream_t s, const char* selftest) {
-  if (!selftest && (!ds.zc_ok || !cfg_.ipc_zc || call.bytes < cfg_.ipc_zc_min)) return 0;
+  if (!selftest && (staged_only_ || !ds.zc_ok || !cfg_.ipc_zc || call.bytes < cfg_.ipc_zc_min)) return 0;
   const size_t body = call.bytes / unit * unit;
   if (body == 0) return 0;
   IpcComm& ic = ds.ipc ? *ds.ipc : ipc(ds);
@@ -973,7 +974,7 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
 void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                                  size_t per_call_max, hipStream_t s, const char* selftest) {
   size_t body = 0;
-  if (!selftest && cfg_.ipc_zc_async && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
+  if (!selftest && !staged_only_ && cfg_.ipc_zc_async && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
       !capturing(s)) {
     // gated launches now, the exchange on the exchange thread (launcher.cpp)
     body = call.bytes / unit * unit;
@@ -1168,6 +1169,9 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   // capped for co-residency anyway)
   if (c == Coll::ALLREDUCE && rccl_can && cfg_.ipc_wide_grid > cfg_.ipc_grid && bytes >= cfg_.rccl_wide_min)
     v.push_back(Algo::IPC_WIDE);
+  // the same IPC protocols without zero copy (zero-copy sizes): measured, not assumed, where the
+  // staging copy beats the per-call record exchange
+  if (zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min) v.push_back(Algo::IPC_STAGED);
   // the push all-reduce (zero-copy sizes): every remote access a write instead of a read
   if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
       bytes > cfg_.ipc_1shot_max)
@@ -1327,7 +1331,10 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   te.valid = true;
   for (size_t k = 0; k < n; ++k) {
     if (is_ipc(cands[k])) {
-      (cands[k] == Algo::IPC ? te.ipc_us : cands[k] == Algo::IPC_WIDE ? te.ipc_wide_us : te.push_us) = med[k];
+      (cands[k] == Algo::IPC          ? te.ipc_us
+       : cands[k] == Algo::IPC_WIDE   ? te.ipc_wide_us
+       : cands[k] == Algo::IPC_STAGED ? te.staged_us
+                                      : te.push_us) = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
     } else if (cands[k] == Algo::RCCL_WIDE) {
       te.wide_us = med[k];
@@ -1344,10 +1351,10 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   if (!cfg_.autotune_file.empty() && rank_ == 0 && te.valid) file_append(key, te, ds);
   if (cfg_.log_level >= 1 && rank_ == 0)
     fprintf(stderr,
-            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us%s"
-            " (%d runs each) -> %s\n",
+            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us,"
+            " ipc_staged %.1f us%s (%d runs each) -> %s\n",
             coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us,
-            te.ipc_wide_us, te.push_us,
+            te.ipc_wide_us, te.push_us, te.staged_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -1397,10 +1404,10 @@ void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, con
   }
   flock(fileno(f), LOCK_EX);
   std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
-               "ipc_wide %.1f, ipc_push %.1f\n",
+               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f\n",
                tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
                algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref), (size_t)1 << std::get<3>(key),
-               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us);
+               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us);
   std::fflush(f);
   flock(fileno(f), LOCK_UN);
   std::fclose(f);
@@ -1423,6 +1430,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.ipc_us = e.ipc_us;
     r.push_us = e.push_us;
     r.ipc_wide_us = e.ipc_wide_us;
+    r.staged_us = e.staged_us;
     r.wide_us = e.wide_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);
@@ -1436,6 +1444,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
 void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko,
                                            ncclDataType_t nd, ncclRedOp_t no, bool nok, RedOpType op, int root,
                                            bool rooted, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -1478,8 +1487,9 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
 
 void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root, DeviceState& ds, hipStream_t s,
                                            std::chrono::milliseconds to) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = w.nbytes();
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
     c.coll = bytes <= cfg_.ipc_1shot_max ? kern::IpcColl::BROADCAST_1SHOT : kern::IpcColl::BROADCAST_2SHOT;
@@ -1513,9 +1523,10 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
 void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const std::vector<at::Tensor>& wo, int root,
                                            bool rooted, DeviceState& ds, hipStream_t s,
                                            std::chrono::milliseconds to) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = wi.nbytes();
   const bool receiver = !rooted || rank_ == root;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
     c.coll = rooted ? kern::IpcColl::GATHER : kern::IpcColl::ALLGATHER;
@@ -1577,8 +1588,9 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
 
 void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& wi, const at::Tensor& wo, int root,
                                          DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = wo.nbytes();
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
     c.coll = kern::IpcColl::SCATTER;
@@ -1630,8 +1642,9 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
                                                 kern::DType kd, kern::RedOp ko, ncclDataType_t nd, ncclRedOp_t no,
                                                 bool nok, RedOpType op, DeviceState& ds, hipStream_t s,
                                                 std::chrono::milliseconds to) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = wo.nbytes();
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
     c.coll = kern::IpcColl::REDUCE_SCATTER;
@@ -1683,7 +1696,8 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
 
 void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>& wi, const std::vector<at::Tensor>& wo,
                                           bool equal, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
-  if (a == Algo::IPC) {
+  const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
+  if (is_ipc(a)) {
     TORCH_CHECK(equal, "pdcc: the IPC all-to-all needs equal splits");
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -1831,7 +1845,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     return cpu_done(Coll::BROADCAST, {t});
   }
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
@@ -1841,7 +1855,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     if (!w.is_same(t) && rank_ != root) t.copy_(w);
   }, icp);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
-  record(Coll::BROADCAST, a == Algo::IPC ? (ll ? "ipc_ll" : one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
+  record(Coll::BROADCAST, is_ipc(a) ? (ll ? "ipc_ll" : one_shot ? "ipc_1shot" : "ipc_2shot") : "rccl", bytes, t0);
   return work;
 }
 
@@ -1890,12 +1904,12 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
   std::vector<at::Tensor> keep{in, wi};
   for (auto& o : wo) keep.push_back(o);
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
   const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
-  const char* algo = a == Algo::IPC ? (ll ? "ipc_ll" : "ipc")
+  const char* algo = is_ipc(a) ? (ll ? "ipc_ll" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
   auto work = gpu_issue(cname, ds, a, keep, outs, to, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
     enqueue_allgather(a, wi, wo, root, rooted, *dsp, x, to);
@@ -1943,7 +1957,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
   std::vector<at::Tensor> keep{out, wo};
   for (auto& i : wi) keep.push_back(i);
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
@@ -1951,7 +1965,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
     enqueue_scatter(a, wi, wo, root, *dsp, x, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  record(Coll::SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl", bytes, t0);
+  record(Coll::SCATTER, is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl", bytes, t0);
   return work;
 }
 
@@ -1999,7 +2013,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
   std::vector<at::Tensor> keep{out, wo};
   for (auto& i : wi) keep.push_back(i);
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
@@ -2008,7 +2022,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, *dsp, x, to);
     if (!wo.is_same(out)) out.copy_(wo);
   }, icp);
-  record(Coll::REDUCE_SCATTER, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
+  record(Coll::REDUCE_SCATTER, is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
          bytes, t0);
   return work;
 }
@@ -2055,7 +2069,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
   for (auto& x : wi) keep.push_back(x);
   for (auto& x : wo) keep.push_back(x);
   std::shared_ptr<IpcComm> icp;
-  if (a == Algo::IPC) {
+  if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
@@ -2064,7 +2078,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
     for (size_t i = 0; i < outs.size(); ++i)
       if (!wo[i].is_same(outs[i])) outs[i].copy_(wo[i]);
   }, icp);
-  record(Coll::ALLTOALL, a == Algo::IPC ? (ds.ll_ok && bytes_in_ll_range(chunk) ? "ipc_ll" : "ipc") : "rccl", total,
+  record(Coll::ALLTOALL, is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(chunk) ? "ipc_ll" : "ipc") : "rccl", total,
          t0);
   return work;
 }

@@ -558,6 +558,7 @@ class ProcessGroupMI355X : public c10d::Backend {
     double push_us;   // push all-reduce (0 = not raced)
     double wide_us;   // RCCL on the wide child communicator (0 = not raced)
     double ipc_wide_us;  // pull all-reduce with ipc_wide_grid workgroups (0 = not raced)
+    double staged_us;    // IPC with zero copy off (0 = not raced)
     bool valid;       // IPC result(s) matched the reference engine's on every rank
     std::string algo;
     int iters;        // timed runs per engine (median taken)
@@ -576,7 +577,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
     Algo ref = Algo::RCCL;
-    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0, ipc_wide_us = 0;
+    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0, ipc_wide_us = 0, staged_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
     int iters = 0;
@@ -584,6 +585,14 @@ class ProcessGroupMI355X : public c10d::Backend {
   // (coll, dtype or -1, reduce op or -1 (copies: list layout), floor(log2 bytes)) -> decision
   using TuneKey = std::tuple<int, int, int, int>;
   std::map<TuneKey, TuneEntry> tune_;
+  // set while an IPC_STAGED enqueue runs (caller's thread): ipc_run stages instead of zero copy
+  bool staged_only_ = false;
+  struct StagedOnly {
+    bool& f;
+    const bool saved;
+    StagedOnly(bool& flag, bool on) : f(flag), saved(flag) { f = on; }
+    ~StagedOnly() { f = saved; }
+  };
   std::mutex tune_mu_;
   std::atomic<bool> tuning_{false};  // an autotune race is running: IPC spin timeouts are its verdict
   // engines worth timing for this call (reference engine first); empty = no tuning

@@ -161,6 +161,7 @@ PYBIND11_MODULE(_C, m) {
                d["push_us"] = r.push_us;
                d["wide_us"] = r.wide_us;
                d["ipc_wide_us"] = r.ipc_wide_us;
+               d["staged_us"] = r.staged_us;
                d["ipc_valid"] = r.valid;
                d["algo"] = r.algo;
                d["iters"] = r.iters;

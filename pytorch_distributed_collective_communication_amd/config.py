@@ -6,7 +6,7 @@ group is constructed; :func:`current` shows what a new group would use and
 
 | variable | default | meaning |
 |---|---|---|
-| PDCC_ALGO | auto | force ``rccl`` / ``rccl_wide`` / ``ipc`` / ``ipc_push`` / ``ipc_wide`` / ``host`` for GPU tensors (preferred if feasible) |
+| PDCC_ALGO | auto | force ``rccl`` / ``rccl_wide`` / ``ipc`` / ``ipc_push`` / ``ipc_wide`` / ``ipc_staged`` (IPC without zero copy) / ``host`` for GPU tensors (preferred if feasible) |
 | PDCC_IPC | 1 | enable the hipIpc peer-memory path |
 | PDCC_IPC_SELFTEST | 1 | run the IPC protocol once on known data when a group first uses a GPU; any failure on any rank disables IPC for that group |
 | PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers (capped by the group timeout) |
@@ -156,8 +156,8 @@ def current(environ=None) -> Config:
         raw = env.get(_ENV[f.name])
         if raw not in (None, ""):
             setattr(c, f.name, _parse(f.type, raw))
-    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "ipc_wide", "host"):
-        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|host, got {c.algo!r}")
+    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "ipc_wide", "ipc_staged", "host"):
+        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|host, got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     if c.rccl_group_comm not in ("share", "split", "init"):

@@ -1444,7 +1444,7 @@ def zc_burst_probe(rank, size, device="cuda", calls=64, n=(4 << 20) // 4):
 
 # elements per case: every size ragged (not a multiple of a 4 KiB tile or of W tiles)
 _NUMERICS_SIZES = {"ll": (1, 777, 16381), "oneshot": (40_009, 100_003), "twoshot": (300_007, 1_000_003),
-                   "zc": (700_001, 2_000_003), "push": (700_001, 2_000_003)}
+                   "zc": (700_001, 2_000_003), "push": (700_001, 2_000_003), "staged_algo": (700_001, 2_000_003)}
 
 
 def random_numerics(rank, size, device="cuda", mode="ll"):

@@ -179,7 +179,7 @@ def test_autotuner_shared_gpu():
     assert los == [64 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20], res[0]["table"]
     for e in res[0]["table"]:
         assert e["coll"] == "allreduce" and e["ipc_valid"], e
-        assert e["algo"] in ("ipc", "ipc_push", "host") and e["ref"] == "host"
+        assert e["algo"] in ("ipc", "ipc_push", "ipc_staged", "host") and e["ref"] == "host"
         assert e["dtype"] in ("Float", "BFloat16") and e["op"] == "SUM", e
         assert e["iters"] >= 3
 
@@ -198,7 +198,7 @@ def test_autotuner_every_collective_shared_gpu():
                  ("allreduce", "Int", "BAND"), ("allreduce", "Int", "BOR")]:
         assert want in rows, (want, sorted(rows))
     for e in res[0]["table"]:
-        assert e["ipc_valid"] and e["algo"] in ("ipc", "ipc_push", "host"), e
+        assert e["ipc_valid"] and e["algo"] in ("ipc", "ipc_push", "ipc_staged", "host"), e
 
 
 def test_autotune_ipc_timeout_is_contained():
@@ -461,6 +461,8 @@ _NUMERICS_ENV = {
                 "ipc_2shot"),
     "zc": ({"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_2shot_zc"),
     "push": ({"PDCC_ALGO": "ipc_push", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_push"),
+    # the autotuner's staged candidate at zero-copy sizes (IPC with zero copy off for the call)
+    "staged_algo": ({"PDCC_ALGO": "ipc_staged", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_2shot"),
 }
 
 
@@ -473,7 +475,7 @@ def test_random_numerics_every_protocol(mode, world):
         bad = {k: v for k, v in r.items() if not v[0]}
         assert not bad, bad
         engines = {v[1] for k, v in r.items() if k.startswith("all_reduce/")}
-        if mode == "twoshot":
+        if mode in ("twoshot", "staged_algo"):
             assert engines == {"ipc_2shot"}, engines
         else:
             assert all(e.startswith(want) for e in engines), engines
