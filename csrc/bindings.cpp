@@ -69,7 +69,8 @@ void reduce_nway(const std::vector<at::Tensor>& srcs, at::Tensor& out, const std
   TORCH_CHECK(e == hipSuccess, "reduce_nway launch failed: ", hipGetErrorString(e));
 }
 
-void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, int max_blocks, int depth) {
+void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts, int max_blocks, int depth,
+                int ntl) {
   TORCH_CHECK(srcs.size() == dsts.size(), "multi_copy: list length mismatch");
   if (srcs.empty()) return;
   std::vector<pdcc::kern::CopyDesc> d;
@@ -83,7 +84,7 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
   }
   c10::hip::HIPGuardMasqueradingAsCUDA g(srcs[0].device());
   hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(srcs[0].device().index()).stream();
-  hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s, max_blocks, depth);
+  hipError_t e = pdcc::kern::multi_copy(d.data(), (int)d.size(), s, max_blocks, depth, ntl);
   TORCH_CHECK(e == hipSuccess, "multi_copy launch failed: ", hipGetErrorString(e));
 }
 
@@ -229,6 +230,7 @@ PYBIND11_MODULE(_C, m) {
         "K1: out = op(srcs...) on the current stream (mode: 1 LDS-DMA engine | 2 non-temporal stores | "
         "4 streaming kernel | 8 non-temporal loads)");
   m.def("multi_copy", &multi_copy, py::arg("srcs"), py::arg("dsts"), py::arg("max_blocks") = 0, py::arg("depth") = 0,
+        py::arg("ntl") = -1,
         "K2: one-launch multi-tensor copy (max_blocks/depth 0 = defaults)");
   m.def("ipc_signal_bytes", &pdcc::kern::ipc_signal_bytes);
   m.def("device_links", &device_links,

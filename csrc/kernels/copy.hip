@@ -42,11 +42,12 @@ struct DescMap {
   __device__ size_t valid(size_t) const { return kTile; }
 };
 
-template <int D>
+// NTL: non-temporal source loads (a pack / unpack reads each source once)
+template <int D, bool NTL>
 __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, D>::kBytes];
   const DescMap m{&a, blockIdx.x, gridDim.x, a.prefix[a.n]};
-  pipe_run<DType::U8, RedOp::COPY, 1, D>(lds, m, 1);
+  pipe_run<DType::U8, RedOp::COPY, 1, D, DescMap, 1, false, NTL>(lds, m, 1);
   // partial last tiles: one block each, bounded plain loads
   for (int k = blockIdx.x; k < a.ntail; k += gridDim.x) {
     const kern::CopyDesc& d = a.d[a.tail_idx[k]];
@@ -285,7 +286,14 @@ static int k2_grid(uint64_t tiles, int ndesc, size_t bytes) {
   return avg >= (16u << 20) ? 256 : 512;
 }
 
-hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks, int depth) {
+// Non-temporal source loads by default for big lists of mid-size tensors (scripts/k2_sweep.py on
+// MI355X, profiles/r3/k2_sweep_ntl_r3.json: 64 x 4 MiB 5.90 vs 5.45 TB/s, 8 x 32 MiB 5.85 vs 5.80);
+// a wash or slightly worse for 128-256 MiB descriptors and for small lists.
+static bool k2_ntl(size_t bytes, int ndesc) {
+  return bytes >= (64u << 20) && bytes / (size_t)std::max(1, ndesc) <= (32u << 20);
+}
+
+hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks, int depth, int ntl_mode) {
   if (depth <= 0) depth = kK2Depth;
   auto aligned = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
   for (int base = 0; base < n; base += kMaxCopyDescs) {
@@ -311,10 +319,16 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
     if (a.n == 0) continue;
     a.prefix[a.n] = acc;
     const int cap = max_blocks > 0 ? max_blocks : k2_grid(acc, a.n, bytes);
+    const bool ntl = ntl_mode < 0 ? k2_ntl(bytes, a.n) : ntl_mode > 0;
     const int grid =
         (int)std::max<uint64_t>(1, std::min<uint64_t>(std::max<uint64_t>(acc, (uint64_t)a.ntail), (uint64_t)cap));
-    if (depth >= 8) hipLaunchKernelGGL(dev::k2_multi_copy<8>, dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL(dev::k2_multi_copy<4>, dim3(grid), dim3(256), 0, stream, a);
+    if (depth >= 8) {
+      if (ntl) hipLaunchKernelGGL((dev::k2_multi_copy<8, true>), dim3(grid), dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((dev::k2_multi_copy<8, false>), dim3(grid), dim3(256), 0, stream, a);
+    } else {
+      if (ntl) hipLaunchKernelGGL((dev::k2_multi_copy<4, true>), dim3(grid), dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((dev::k2_multi_copy<4, false>), dim3(grid), dim3(256), 0, stream, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

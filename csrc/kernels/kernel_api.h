@@ -71,7 +71,9 @@ constexpr int kK2Depth = 4;        // K2 default LDS-DMA ring depth (tiles in fl
 // One launch copies every descriptor (pack = many->one, unpack = one->many).
 // max_blocks / depth: 0 = defaults (grid from the list's shape, see k2_grid in copy.hip;
 // kK2Depth tiles in flight per workgroup)
-hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks = 0, int depth = 0);
+// ntl_mode: non-temporal source loads (1 on, 0 off, -1 = by the list's shape)
+hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_blocks = 0, int depth = 0,
+                      int ntl_mode = -1);
 
 // ---------------------------------------------------------------- IPC collectives
 // Per-rank view of the group's registered (hipIpc) memory for ONE call.

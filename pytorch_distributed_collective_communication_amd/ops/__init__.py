@@ -84,12 +84,13 @@ def reduce_nway_reference(srcs: Sequence[torch.Tensor], op: str = "sum") -> torc
 
 
 def multi_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor], max_blocks: int = 0,
-               depth: int = 0) -> None:
+               depth: int = 0, ntl: bool | None = None) -> None:
     """K2: copy srcs[i] -> dsts[i] for every i in ONE kernel launch.
 
     ``max_blocks`` caps the grid and ``depth`` (4 or 8) sets the LDS-DMA ring
-    depth; 0 keeps the tuned defaults (csrc/kernels/kernel_api.h kK2Grid/kK2Depth)."""
-    _C().multi_copy(list(srcs), list(dsts), max_blocks, depth)
+    depth; 0 keeps the tuned defaults (csrc/kernels/kernel_api.h kK2Grid/kK2Depth); ``ntl``
+    forces non-temporal source loads on / off (None: by the list's shape, see k2_ntl in copy.hip)."""
+    _C().multi_copy(list(srcs), list(dsts), max_blocks, depth, -1 if ntl is None else int(bool(ntl)))
 
 
 def _byte_view(t: torch.Tensor) -> torch.Tensor:

@@ -40,8 +40,12 @@ for count, nbytes in shapes:
     for _ in range(3):
         for depth in (4, 8):
             for g in (256, 512, 1024, 2048):
-                t = timeit(lambda: ops.multi_copy(srcs, dsts, max_blocks=g, depth=depth))
+                t = timeit(lambda: ops.multi_copy(srcs, dsts, max_blocks=g, depth=depth, ntl=False))
                 res.setdefault(f"{tag}_d{depth}_g{g}", []).append(byts / t / 1e9)
+        t = timeit(lambda: ops.multi_copy(srcs, dsts, ntl=False))
+        res.setdefault(f"{tag}_default_grid", []).append(byts / t / 1e9)
+        t = timeit(lambda: ops.multi_copy(srcs, dsts, ntl=True))
+        res.setdefault(f"{tag}_default_grid_ntl", []).append(byts / t / 1e9)
         t = timeit(lambda: ops.multi_copy(srcs, dsts))
         res.setdefault(f"{tag}_default", []).append(byts / t / 1e9)
         t = timeit(lambda: flat_dst.copy_(flat_src))
