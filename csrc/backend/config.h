@@ -41,10 +41,12 @@ struct Config {
   // reduce locally and write the result into every rank's tensor) for zero-copy sizes.
   bool ipc_push = true;                    // PDCC_IPC_PUSH
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
-  // All-reduces up to this size (<= 64 KiB, kern::kLLMaxBytes) use the LL protocol: every
+  // All-reduces up to this size (<= 256 KiB, kern::kLLMaxBytes) use the LL protocol: every
   // rank pushes flag-tagged 8-byte words into its peers' signal areas and polls its own --
   // no staging copy and no barrier (0 = off; gated by its own self-test).
-  size_t ipc_ll_max = 64u << 10;           // PDCC_IPC_LL_MAX
+  // (256 KiB: LL beats the staged protocols at 128-256 KiB on MI355X, 8.1 vs 14.9 us per 256 KiB
+  // all_reduce at W = 2, 11.6 vs 23.7 at W = 4: profiles/r3/ll_bench_256k_r3.jsonl)
+  size_t ipc_ll_max = 256u << 10;          // PDCC_IPC_LL_MAX
   size_t ipc_zc_cache = 16;                // PDCC_IPC_ZC_CACHE
   // Zero-copy calls exchange their records on a per-device launcher thread (IpcLauncher in
   // process_group.h): the caller's host never waits for its peers (0 = inline exchange)

@@ -95,7 +95,7 @@ constexpr int kEpochsPerCall = 4;                   // arrival, data, second dat
 // block that finishes last (ctl[0] = epoch of the last finished call, ctl[1] = exit count).
 constexpr int kLLCtlWord = kCountWord + kMaxBlocks;        // u32 index of ctl[0] in the signal area
 constexpr size_t kLLOffset = 40960;                        // byte offset of the receive slots
-constexpr size_t kLLMaxBytes = 64u << 10;                  // payload per rank of one LL call
+constexpr size_t kLLMaxBytes = 256u << 10;                 // payload per rank of one LL call (cap of PDCC_IPC_LL_MAX)
 constexpr size_t kLLSlotBytes = 2 * kLLMaxBytes;           // 8-byte words of 4 data bytes
 static_assert(kLLOffset >= (size_t)(kLLCtlWord + 16) * 4, "LL slots overlap the signal words");
 // The view and call structs are templates over the pointer type P<T>: the host (and the

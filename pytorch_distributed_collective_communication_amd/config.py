@@ -17,7 +17,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_MAX_STAGING | 1G | staging bytes; larger calls are chunked |
 | PDCC_IPC_SPIN_MS | 600000 | bound on one cross-GPU barrier spin of the IPC kernels (the group timeout applies if shorter) |
 | PDCC_IPC_ZC_ASYNC | 1 | zero-copy calls exchange their buffer records on a per-device launcher thread: the caller's host never waits for its peers (0: inline exchange) |
-| PDCC_IPC_LL_MAX | 64K | all-reduces up to this size (max 64K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
+| PDCC_IPC_LL_MAX | 256K | collectives up to this size per rank / chunk (max 256K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
@@ -82,7 +82,7 @@ class Config:
     ipc_zc: bool = True
     ipc_push: bool = True
     ipc_zc_min: int = 1 << 20
-    ipc_ll_max: int = 64 << 10
+    ipc_ll_max: int = 256 << 10
     ipc_zc_cache: int = 16
     ipc_zc_async: bool = True
     ipc_spin_ms: int = 600000

@@ -3,7 +3,7 @@
 
 Ranks share ONE GPU on the 1-GPU boxes (PDCC_ALGO=ipc), so this measures the
 protocols' own cost (flag round trips, staging copy, barriers), not xGMI latency.
-`--modes ll,oneshot`: ll = default (PDCC_IPC_LL_MAX=64K), oneshot = PDCC_IPC_LL_MAX=0.
+`--modes ll,oneshot`: ll = PDCC_IPC_LL_MAX=--ll-max (default 64K), oneshot = PDCC_IPC_LL_MAX=0.
 Per (mode, size): median over `--iters` of one isolated synchronous all_reduce, end to
 end (host call + kernel + the ranks' arrival skew), and the per-call time of 50
 back-to-back calls (median of 5), max over ranks. One JSON line per mode.
@@ -122,12 +122,13 @@ def main():
     ap.add_argument("--sizes", default="4,1K,16K,64K")
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--modes", default="ll,oneshot")
+    ap.add_argument("--ll-max", default="64K", help="PDCC_IPC_LL_MAX of the ll mode (<= 256K)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     sizes = [parse_size(s) for s in a.sizes.split(",")]
     for mode in a.modes.split(","):
-        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_MAX": "64K" if mode == "ll" else "0"}
+        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_LL_MAX": a.ll_max if mode == "ll" else "0"}
         res = launch(work, a.world, args=(sizes, a.iters), bind_device=True, timeout_s=120, env=env,
                      join_timeout_s=600)
         print(json.dumps({"mode": mode, "world": a.world, **res[0]}), flush=True)

@@ -171,7 +171,8 @@ def test_async_ops_stream_ordering(world, stream):
 def test_autotuner_shared_gpu():
     # ranks share one GPU, so RCCL is out: the tuner weighs IPC against the host
     # transport for buckets <= 4 MiB and leaves 16 MiB to the static choice
-    res = _gpu_launch(W.autotune_probe, 2, env={"PDCC_LOG_LEVEL": "1"})
+    # (LL capped at 64 KiB: the probe's smallest size is the first tuned bucket above it)
+    res = _gpu_launch(W.autotune_probe, 2, env={"PDCC_LOG_LEVEL": "1", "PDCC_IPC_LL_MAX": "64K"})
     for r in res:
         assert all(r["ok"]), r["ok"]
     assert res[0]["table"] == res[1]["table"]
@@ -187,7 +188,7 @@ def test_autotuner_shared_gpu():
 def test_autotuner_every_collective_shared_gpu():
     # every tunable collective gets its own measured decision (verdict r1 #4), keyed by
     # dtype and op too (an int BAND must not inherit a float SUM decision)
-    res = _gpu_launch(W.autotune_all_colls, 2)
+    res = _gpu_launch(W.autotune_all_colls, 2, env={"PDCC_IPC_LL_MAX": "64K"})  # 256 KiB keys: tuned, not LL
     for r in res:
         assert all(r["ok"].values()), r["ok"]
     assert res[0]["table"] == res[1]["table"]
@@ -485,7 +486,7 @@ def test_autotune_file_persists_decisions(tmp_path):
     # verdict r2 weak #8: PDCC_AUTOTUNE_FILE -- the first run races every key and rank 0 appends
     # the verdicts; a second run on the same topology takes them from the file, no race (iters 0)
     f = tmp_path / "tune.txt"
-    env = {"PDCC_AUTOTUNE_FILE": str(f)}
+    env = {"PDCC_AUTOTUNE_FILE": str(f), "PDCC_IPC_LL_MAX": "64K"}
     first = _gpu_launch(W.autotune_probe, 2, env=env)
     assert all(first[0]["ok"]) and all(first[1]["ok"])
     lines = [ln for ln in f.read_text().splitlines() if ln.startswith("pdcc-tune v1 w2-shared-gfx950")]

@@ -63,7 +63,7 @@ def test_rccl_and_ipc_agree_on_random_data():
 
 
 def test_autotuner_distinct_gpus():
-    res = _run(W.autotune_all_colls, 2)
+    res = _run(W.autotune_all_colls, 2, env={"PDCC_IPC_LL_MAX": "64K"})  # 256 KiB keys: tuned, not LL
     for r in res:
         assert all(r["ok"].values()), r["ok"]
     assert res[0]["table"] == res[1]["table"]
