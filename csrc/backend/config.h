@@ -125,8 +125,11 @@ struct Config {
   size_t shm_slot_bytes = 8u << 20;        // PDCC_SHM_SLOT_BYTES
   size_t shm_chan_bytes = 1u << 20;        // PDCC_SHM_CHAN_BYTES
   int shm_spin_us = 300;                   // PDCC_SHM_SPIN_US (busy-wait window before futex sleep)
-  // the zero-copy exchange thread spins this long after its last job before it sleeps
-  int xchg_spin_us = 500;                  // PDCC_XCHG_SPIN_US (0: sleep at once)
+  // the zero-copy exchange thread spins this long after its last job before it sleeps (0: at
+  // once). Off by default: in steady state the kernels resolve zero-copy buffers on the device
+  // and the thread is off the critical path; a spinning thread costs CPU quota (measured on a
+  // 16-CPU box share: 500 us of spin made the host-gated exchange slower, profiles/r3/zx/)
+  int xchg_spin_us = 0;                    // PDCC_XCHG_SPIN_US
   // robustness / observability
   bool debug = false;                      // PDCC_DEBUG=1: cross-rank op fingerprint check
   int log_level = 0;                       // PDCC_LOG_LEVEL 0 quiet, 1 info, 2 every collective

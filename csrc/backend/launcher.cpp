@@ -41,10 +41,10 @@ void ProcessGroupMI355X::launcher_loop(DeviceState* dsp, IpcLauncher* lp) {
   (void)hipSetDevice(ds.device);
   // never a device-synchronising release on this thread (kernels wait for its exchanges)
   IpcComm::set_thread_defers_frees(true);
-  // Zero-copy calls come back to back, and every gated kernel waits for its job: a thread
-  // woken from a condition-variable sleep (measured 60-200 us per job on a busy box, r3
-  // host_path) would put that wake-up into every call. So the thread spins for
-  // PDCC_XCHG_SPIN_US after its last job before it sleeps.
+  // A gated kernel whose buffers are not in the device-side mapping table waits for its job,
+  // and a thread woken from a condition-variable sleep costs 60-200 us per job on a busy box
+  // (r3 host_path): PDCC_XCHG_SPIN_US lets the thread spin that long after its last job before
+  // it sleeps (default 0: in steady state the kernels do not wait for the thread at all).
   const auto spin = std::chrono::microseconds(std::max(0, cfg_.xchg_spin_us));
   uint64_t seen = 0;
   for (;;) {

@@ -37,7 +37,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_SHM_SLOT_BYTES | 8M | host transport staging slot per rank |
 | PDCC_SHM_CHAN_BYTES | 1M | host transport p2p ring per directed pair |
 | PDCC_SHM_SPIN_US | 300 | host transport busy-wait window before a futex sleep (20 when ranks > CPUs) |
-| PDCC_XCHG_SPIN_US | 500 | the zero-copy exchange thread busy-waits this long for the next job before it sleeps (a wake-up per call would delay every gated kernel) |
+| PDCC_XCHG_SPIN_US | 0 | the zero-copy exchange thread busy-waits this long for the next job before it sleeps (steady-state zero-copy calls resolve their buffers on the device, so the thread is off the critical path) |
 | PDCC_STREAM | auto | GPU stream policy: auto (sync ops on the caller's stream, async on a comm stream), high, comm, current |
 | PDCC_DEBUG | 0 | cross-rank fingerprint check before every collective |
 | PDCC_LOG_LEVEL | 0 | 1: group/device info, 2: every collective |
@@ -108,7 +108,7 @@ class Config:
     shm_slot_bytes: int = 8 << 20
     shm_chan_bytes: int = 1 << 20
     shm_spin_us: int = 300
-    xchg_spin_us: int = 500
+    xchg_spin_us: int = 0
     stream: str = "auto"
     debug: bool = False
     log_level: int = 0
