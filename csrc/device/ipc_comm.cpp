@@ -449,6 +449,10 @@ void IpcComm::reap_closing(bool wait_all) {
     if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
     if (c.map) hipIpcCloseMemHandle(c.map);
   }
+  if (!done.empty()) {
+    std::lock_guard<std::mutex> lk(closing_mu_);
+    for (auto& c : done) tab_release(c.tab_peer, c.tab_slot);
+  }
 }
 
 bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
@@ -467,7 +471,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
       auto last = latest_gated();  // ... and the ones launched so far may still read through it
       last.push_back(it->last);
       std::lock_guard<std::mutex> lk(closing_mu_);
-      zc_closing_.push_back({it->map, std::move(last)});
+      zc_closing_.push_back({it->map, std::move(last), it->tab >= 0 ? r : -1, it->tab});
     }
     peer.erase(it);
   }
@@ -558,8 +562,10 @@ uint64_t IpcComm::gate_reserve() {
 
 int IpcComm::tab_insert(int peer, uint64_t id, void* map) {
   if (!ztab_host_ || peer < 0 || peer >= kern::kMaxRanks) return -1;
+  std::lock_guard<std::mutex> lk(closing_mu_);
   for (int j = 0; j < kern::kZcTab; ++j) {
-    if (__atomic_load_n(&ztab_host_->id[peer][j], __ATOMIC_ACQUIRE) != 0) continue;
+    if (tab_busy_[peer][j]) continue;  // (a dropped slot stays busy until its mapping is closed)
+    tab_busy_[peer][j] = true;
     __atomic_store_n(&ztab_host_->base[peer][j], reinterpret_cast<uint64_t>(map), __ATOMIC_RELAXED);
     __atomic_store_n(&ztab_host_->id[peer][j], id, __ATOMIC_RELEASE);  // last: the kernels match on it
     return j;
@@ -570,7 +576,12 @@ int IpcComm::tab_insert(int peer, uint64_t id, void* map) {
 void IpcComm::tab_drop(int peer, int slot) {
   if (!ztab_host_ || slot < 0) return;
   __atomic_store_n(&ztab_host_->id[peer][slot], 0ull, __ATOMIC_RELEASE);
-  __atomic_store_n(&ztab_host_->base[peer][slot], 0ull, __ATOMIC_RELEASE);  // (kernels recheck id after base)
+}
+
+void IpcComm::tab_release(int peer, int slot) {
+  if (!ztab_host_ || peer < 0 || slot < 0) return;
+  __atomic_store_n(&ztab_host_->base[peer][slot], 0ull, __ATOMIC_RELEASE);
+  tab_busy_[peer][slot] = false;
 }
 
 uint32_t IpcComm::zx_verdict(uint64_t tag) {
@@ -579,7 +590,7 @@ uint32_t IpcComm::zx_verdict(uint64_t tag) {
   const char* slot = reinterpret_cast<const char*>(my_flags_) + kern::kZxResolvedOffset +
                      (tag % kern::kGateSlots) * sizeof(kern::GateSlot);
   PDCC_HIP(hipMemcpy(&r, slot, sizeof(r), hipMemcpyDeviceToHost));
-  return r.seq == tag ? r.ok : 0xffffffffu;
+  return (r.seq >> 2) == tag ? (uint32_t)(r.seq & 3u) : 0xffffffffu;  // (seq = tag << 2 | verdict)
 }
 
 std::vector<std::shared_ptr<IpcComm::LaunchEvent>> IpcComm::latest_gated() {

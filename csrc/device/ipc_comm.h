@@ -213,8 +213,10 @@ class IpcComm {
   kern::ZcTable* ztab_dev_ = nullptr;
   std::mutex latest_mu_;
   std::vector<std::pair<hipStream_t, std::shared_ptr<LaunchEvent>>> latest_gated_;
+  bool tab_busy_[kern::kMaxRanks][kern::kZcTab] = {};  // guarded by closing_mu_
   int tab_insert(int peer, uint64_t id, void* map);
-  void tab_drop(int peer, int slot);
+  void tab_drop(int peer, int slot);     // id = 0 (the base stays until the slot is released)
+  void tab_release(int peer, int slot);  // after the mapping closed (closing_mu_ held)
   std::vector<std::shared_ptr<LaunchEvent>> latest_gated();
   // Evicted mappings are closed once the last launch that used them has finished (polled
   // at every exchange; the destructor waits): no device-wide synchronisation, so compute
@@ -222,6 +224,7 @@ class IpcComm {
   struct Closing {
     void* map;
     std::vector<std::shared_ptr<LaunchEvent>> last;  // every launch that may still read through it
+    int tab_peer = -1, tab_slot = -1;  // its mapping-table slot, reusable once the mapping is closed
   };
   mutable std::mutex closing_mu_;
   std::vector<Closing> zc_closing_;

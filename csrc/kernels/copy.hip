@@ -207,7 +207,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
-  stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_copy_body<W>(sv, sc, lds, tr);
   tr.finish(v);

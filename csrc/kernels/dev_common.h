@@ -554,6 +554,9 @@ __device__ __forceinline__ kern::GateSlot* zx_resolved(const kern::IpcView& v, u
   return reinterpret_cast<kern::GateSlot*>(reinterpret_cast<char*>(v.flags[v.rank]) + kern::kZxResolvedOffset) +
          (seq % kern::kGateSlots);
 }
+__device__ __forceinline__ uint64_t zx_tagged(uint64_t tag, uint64_t ptr) {
+  return ((tag & 0xffffull) << 48) | (ptr & 0xffffffffffffull);
+}
 __device__ __forceinline__ void zx_put(uint64_t* p, uint32_t data, uint32_t tag) {
   __hip_atomic_store(p, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -562,7 +565,7 @@ __device__ __forceinline__ void zx_put(uint64_t* p, uint32_t data, uint32_t tag)
 // up in this process's mapping table, vote, and publish the verdict in this call's resolved
 // slot (ok = 1 with the buffers, 2 = wait for the host gate, 0 = a peer never came: staged,
 // the error word is set). Returns nothing; every block reads the resolved slot.
-__device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::IpcCall& c) {
+__device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::IpcCall& c, const PhaseTrace& tr) {
   const int lane = threadIdx.x & 63, W = v.world, me = v.rank;
   uint32_t* epw = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(v.flags[me]) + kern::kZxEpochOffset);
   uint32_t ep = 0;
@@ -604,42 +607,54 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
     }
     __builtin_amdgcn_s_sleep(1);
   }
-  // lookup: lanes 0-31 scan table row q = 2p, lanes 32-63 row 2p + 1 (loads issued together)
+  tr.mark(8);
+  // lookup: lanes 0-31 scan table row q = 2p, lanes 32-63 row 2p + 1; ids and bases loaded in
+  // one pass (a slot's base stays put until its mapping is closed, after every launch that
+  // could have read the entry: an id match never pairs with another mapping's base)
   const kern::ZcTable* tab = c.ztab;
   const int half = lane >> 5, j = lane & 31;
-  uint64_t cand[4];
+  uint64_t cand[4], cbase[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const int q = 2 * p + half;
-    cand[p] = (alive && q < W && q != me)
-                  ? __hip_atomic_load(&tab->id[q][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                  : 0ull;
+    const bool look = alive && q < W && q != me;
+    cand[p] = look ? __hip_atomic_load(&tab->id[q][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+    cbase[p] = look ? __hip_atomic_load(&tab->base[q][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
   }
-  uint64_t masks[4];
+  uint64_t masks[4], bases[4];
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const uint64_t want = __shfl(id, 2 * p + half);  // row q's record id (lane q holds it)
-    masks[p] = __ballot(want != 0ull && want != kern::kZxNoExport && cand[p] == want);
+    const bool hit = want != 0ull && want != kern::kZxNoExport && cand[p] == want && cbase[p] != 0ull;
+    masks[p] = __ballot(hit);
+    // the matching lane's base, broadcast per half (lanes without a hit contribute 0)
+    bases[p] = hit ? cbase[p] : 0ull;
   }
   uint64_t ptr = 0;
   bool found = true;
+  uint64_t base_q = 0;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    // lane q (= 2p + h) takes the base from the first matching lane of half h
+    const uint64_t m0 = masks[p] & 0xffffffffull, m1 = masks[p] >> 32;
+    const int src0 = m0 ? __builtin_ctzll(m0) : 0, src1 = m1 ? 32 + __builtin_ctzll(m1) : 32;
+    const uint64_t b0 = __shfl(bases[p], src0), b1 = __shfl(bases[p], src1);
+    if (lane == 2 * p) base_q = m0 ? b0 : 0ull;
+    if (lane == 2 * p + 1) base_q = m1 ? b1 : 0ull;
+  }
   if (lane < W) {
-    const uint64_t m = masks[lane >> 1] >> ((lane & 1) * 32) & 0xffffffffull;
     if (lane == me) {
       ptr = (uint64_t)(uintptr_t)static_cast<char*>(c.zx_self);
     } else if (id == 0ull) {
       ptr = 0;  // this peer shares nothing in this call
-    } else if (m != 0ull) {
-      const int jj = __builtin_ctzll(m);
-      const uint64_t base = __hip_atomic_load(&tab->base[lane][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      // the entry may have been dropped since the id load: recheck after reading base
-      found = base != 0ull && __hip_atomic_load(&tab->id[lane][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == id;
-      ptr = base + off;
+    } else if (base_q != 0ull) {
+      ptr = base_q + off;
     } else {
       found = false;
     }
   }
   const bool mine_ok = alive && __all(found);
+  tr.mark(9);
   // round 2: the vote (word 4 of slot [me] at every rank)
   bool all_ok = mine_ok;
   if (alive) {
@@ -664,21 +679,22 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
     }
     all_ok = alive && __all(yes);
   }
+  tr.mark(10);
   if (!alive && lane == 0) __hip_atomic_store(v.err, 0x800u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  // publish for the kernel's blocks (uncached signal memory: relaxed words, seq last)
+  // publish for the kernel's blocks: every word carries this launch's tag (ptr words in their
+  // top 16 bits -- virtual addresses are 48-bit -- the verdict as seq = tag << 2 | verdict), so
+  // readers check each word and no write ordering (no fence) is needed
   kern::GateSlot* res = zx_resolved(v, c.zx_tag);
+  const uint32_t verdict = !alive ? 0u : (all_ok ? 1u : 2u);
   if (lane < kern::kMaxRanks)
-    __hip_atomic_store(&res->ptr[lane], (all_ok && lane < W) ? ptr : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&res->ptr[lane], zx_tagged(c.zx_tag, (all_ok && lane < W) ? ptr : 0ull), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  tr.mark(11);
   if (lane == 0) {
-    __hip_atomic_store(&res->ok, !alive ? 0u : (all_ok ? 1u : 2u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (lane == 0) {
-    __hip_atomic_store(&res->seq, c.zx_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&res->seq, (c.zx_tag << 2) | verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // for the host's statistics (read when the gate slot is reused): a posted store, off the critical path
-    __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), 0x100u | (!alive ? 0u : (all_ok ? 1u : 2u)),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), 0x100u | verdict, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -688,8 +704,21 @@ __device__ __forceinline__ bool zx_wait(const kern::IpcView& v, const kern::IpcC
                                         uint64_t (&ptrs)[kern::kMaxRanks]) {
   kern::GateSlot* res = zx_resolved(v, c.zx_tag);
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t want = (c.zx_tag & 0xffffull) << 48;
   for (uint32_t it = 1;; ++it) {
-    if (__hip_atomic_load(&res->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == c.zx_tag) break;
+    const uint64_t sq = __hip_atomic_load(&res->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((sq >> 2) == c.zx_tag) {
+      bool all = true;
+      for (int r = 0; r < v.world; ++r) {
+        const uint64_t w = __hip_atomic_load(&res->ptr[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        all = all && (w & ~0xffffffffffffull) == want;
+        ptrs[r] = w & 0xffffffffffffull;
+      }
+      if (all) {
+        ok = (uint32_t)(sq & 3u);
+        return true;
+      }
+    }
     if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
       __hip_atomic_store(v.err, 0x1000u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
@@ -697,13 +726,11 @@ __device__ __forceinline__ bool zx_wait(const kern::IpcView& v, const kern::IpcC
     if ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return false;
     __builtin_amdgcn_s_sleep(1);
   }
-  ok = __hip_atomic_load(&res->ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int r = 0; r < kern::kMaxRanks; ++r) ptrs[r] = __hip_atomic_load(&res->ptr[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
 }
 
-__device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, DView& sv, DCall& sc) {
-  if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x < 64) zx_resolve(v, c);
+__device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, DView& sv, DCall& sc,
+                                           const PhaseTrace& tr) {
+  if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x < 64) zx_resolve(v, c, tr);
   if (threadIdx.x == 0) {
     __builtin_memcpy(&sv, &v, sizeof(DView));  // same layout, pointers retyped global
     __builtin_memcpy(&sc, &c, sizeof(DCall));

@@ -125,8 +125,10 @@ using IpcView = IpcViewT<RawPtr>;
 // Device-side phase trace of an IPC call (block 0, s_memrealtime ticks at 100 MHz):
 // [0] block 0's call number, [1] entry, [2] arrival barrier passed, [3] local data
 // staged (a gated launch: its gate passed), [4] data barrier passed, [5] first pull / reduce done, [6] second data
-// barrier passed (2-shot), [7] exit. Record `seq % trace_cap`.
-constexpr int kTraceWords = 8;
+// barrier passed (2-shot), [7] exit; a gated zero-copy launch's device-side exchange (block 0):
+// [8] every rank's record in, [9] mapping lookup done, [10] every vote in, [11] verdict published.
+// Record `seq % trace_cap`.
+constexpr int kTraceWords = 12;
 
 enum class IpcColl : int32_t {
   ALLREDUCE_1SHOT = 0,   // stage, barrier, every rank reduces everything from all peers

@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
-  stage_args(v, c, sv, sc);  // (a gated zero-copy launch waits for its buffers here)
+  stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);
   tr.finish(v);

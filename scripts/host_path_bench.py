@@ -73,6 +73,11 @@ def work(rank, size, calls, trace=False):
                 out_trace = {"calls": len(recs), "entry_to_arrival_us": med([r[2] - r[1] for r in recs if r[2]]),
                              "gated_calls": len(gated),
                              "gate_wait_us": med([r[3] - r[1] for r in gated]) if gated else None,
+                             # device-side exchange phases (block 0): records in / lookup / votes / published
+                             "zx_records_us": med([r[8] - r[1] for r in gated if r[8]]) if gated else None,
+                             "zx_lookup_us": med([r[9] - r[8] for r in gated if r[9]]) if gated else None,
+                             "zx_vote_us": med([r[10] - r[9] for r in gated if r[10]]) if gated else None,
+                             "zx_publish_us": med([r[11] - r[10] for r in gated if r[11]]) if gated else None,
                              "arrival_to_exit_us": med([r[7] - r[2] for r in recs if r[2]]),
                              "kernel_us": med([r[7] - r[1] for r in recs])}
         m = re.search(r"launcher_jobs=(\d+).*?xchg_wait_us=(\d+), xchg_us=(\d+), xchg_gather_us=(\d+), "
