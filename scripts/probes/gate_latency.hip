@@ -1,3 +1,4 @@
+// build: hipcc --offload-arch=gfx950 -O2 scripts/probes/gate_latency.hip -o scripts/probes/gate_latency
 // Probe: device-side cost of the zero-copy gate poll (dev_common.h gate_wait) on MI355X.
 // Times, with s_memrealtime (100 MHz), (a) one system-scope acquire load of pinned coherent
 // host memory, (b) the same of device memory, (c) s_sleep(4) and s_sleep(127), and (d) how
