@@ -42,6 +42,26 @@ BASELINE_P50_MS = {1: 0.027, 2: 174.8, 4: 293.4, 8: 595.1}  # same table, p50 la
 SMALL = os.environ.get("PDCC_BENCH_SMALL", "0") == "1"  # functional rehearsal sizes for the extras
 NBYTES = 1 << 30
 EXTRAS_PARTIAL: dict = {}  # run_extras fills this in place (reported even if a deadline fires)
+# wall seconds per section of this rank's run (extras.timing; rank 0's view): on the first
+# multi-GPU node every first call pays for communicators, self-tests and autotune races
+TIMING: dict = {}
+EXTRAS_PARTIAL["timing"] = TIMING
+T_START = time.time()
+
+
+class section:
+    """``with section("name"):`` adds the block's wall seconds to extras.timing[name]."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.time()
+        return self
+
+    def __exit__(self, *exc):
+        TIMING[self.name] = round(TIMING.get(self.name, 0.0) + time.time() - self.t0, 3)
+        return False
 
 
 def busbw(nbytes: int, n: int, sec: float) -> float:
@@ -84,7 +104,8 @@ def launch_ranks(n: int, argv) -> int:
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
-    deadline = time.time() + float(os.environ.get("PDCC_BENCH_TIMEOUT_S", "1500"))
+    # below the driver's own 600 s limit: if the ranks hang, this parent (not the driver) stops them
+    deadline = time.time() + float(os.environ.get("PDCC_BENCH_TIMEOUT_S", "540"))
     rc = 0
     while True:
         codes = [p.poll() for p in procs]
@@ -141,8 +162,22 @@ def run_rank(args):
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     on_gpu = os.environ.get("PDCC_BENCH_DEVICE", "cuda") != "cpu"
+    TIMING["startup"] = round(time.time() - T_START, 3)
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
+    # the job's store first (torch's own env:// rendezvous, agent store under torchrun): the
+    # RCCL environment pre-sweep below runs over it before this process touches the GPU
+    with section("rendezvous"):
+        from torch.distributed import rendezvous
+
+        store, _, _ = next(rendezvous("env://", rank, world, timeout=datetime.timedelta(minutes=10)))
+    # counting devices does not initialise the GPU on this runtime; set_device does
+    ngpu = torch.cuda.device_count() if on_gpu else 0
+    with section("rccl_env_sweep"):
+        EXTRAS_PARTIAL["rccl_env_sweep"] = rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args)
     if on_gpu:
-        ngpu = torch.cuda.device_count()
         local = local % ngpu  # (ranks > GPUs only in functional rehearsals on a 1-GPU box)
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -150,11 +185,9 @@ def run_rank(args):
         dev = torch.device("cpu")
         torch.set_num_threads(1)
     csync = torch.cuda.synchronize if on_gpu else (lambda: None)
-    if world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if "MASTER_PORT" not in os.environ:
-            os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("mi355x", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=10))
+    with section("init_process_group"):
+        dist.init_process_group("mi355x", store=store, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(minutes=10))
     native = be.native_backend()
 
     numel = args.bytes // 4
@@ -174,44 +207,54 @@ def run_rank(args):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)  # CPU tensor: host transport
         return t.item()
 
-    for _ in range(args.warmup):
-        dist.all_reduce(x)
-    x.copy_(x0)
-    sync()
+    # warm-up; the first call sets the GPU path up (topology, IPC self-test, communicators,
+    # the autotune race for this size) and is timed on its own
+    with section("first_call"):
+        if args.warmup > 0:
+            dist.all_reduce(x)
+        csync()
+    with section("warmup"):
+        for _ in range(max(0, args.warmup - 1)):
+            dist.all_reduce(x)
+        x.copy_(x0)
+        sync()
     if rank == 0:
         print(f"[bench] world={world} warm-up done, timing {args.steps} steps", file=sys.stderr, flush=True)
     # ---- the timed region: exactly K steps
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dist.all_reduce(x)
-    algo = native.last_algo() or "?"  # the engine that served the timed steps
-    csync()
-    dist.barrier()
-    csync()
-    total = max_over_ranks(time.perf_counter() - t0)
+    with section("timed"):
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dist.all_reduce(x)
+        algo = native.last_algo() or "?"  # the engine that served the timed steps
+        csync()
+        dist.barrier()
+        csync()
+        total = max_over_ranks(time.perf_counter() - t0)
     finite = bool(torch.isfinite(x).all().item())
     ms_per_step = total / args.steps * 1e3
 
     # ---- p50 of individually bracketed steps (BASELINE.md method)
-    lat = []
-    for _ in range(args.steps):
+    with section("p50_steps"):
+        lat = []
+        for _ in range(args.steps):
+            x.copy_(x0)
+            sync()
+            s0 = time.perf_counter()
+            dist.all_reduce(x)
+            csync()
+            lat.append(max_over_ranks(time.perf_counter() - s0))
+        p50 = statistics.median(lat)
+        finite = finite and bool(torch.isfinite(x).all().item())
         x.copy_(x0)
-        sync()
-        s0 = time.perf_counter()
-        dist.all_reduce(x)
-        csync()
-        lat.append(max_over_ranks(time.perf_counter() - s0))
-    p50 = statistics.median(lat)
-    finite = finite and bool(torch.isfinite(x).all().item())
-    x.copy_(x0)
-    del x0
+        del x0
 
     # ---- correctness of the headline path
-    y = torch.full((numel,), float(rank + 1), device=dev)
-    dist.all_reduce(y)
-    exp = world * (world + 1) / 2
-    correct = bool(torch.all(y == exp).item())
-    del y
+    with section("correctness"):
+        y = torch.full((numel,), float(rank + 1), device=dev)
+        dist.all_reduce(y)
+        exp = world * (world + 1) / 2
+        correct = bool(torch.all(y == exp).item())
+        del y
 
     value = busbw(args.bytes, world, ms_per_step / 1e3)
     try:  # the autotuner's decisions for the headline path (size bucket -> engine, times)
@@ -276,9 +319,10 @@ def run_rank(args):
             from pytorch_distributed_collective_communication_amd.utils import conformance
 
             progress("conformance pass")
-            EXTRAS_PARTIAL["conformance"] = conformance.run(
-                rank, world, dev, deadline_s=float(os.environ.get("PDCC_BENCH_CONFORMANCE_S", "45")),
-                max_bytes=(64 << 20) if on_gpu and not SMALL else (1 << 20))
+            with section("conformance"):
+                EXTRAS_PARTIAL["conformance"] = conformance.run(
+                    rank, world, dev, deadline_s=float(os.environ.get("PDCC_BENCH_CONFORMANCE_S", "45")),
+                    max_bytes=(64 << 20) if on_gpu and not SMALL else (1 << 20))
         except Exception as e:
             EXTRAS_PARTIAL["conformance"] = {"all_ok": False, "error": f"{type(e).__name__}: {e}"[:500]}
         if on_gpu:
@@ -288,13 +332,43 @@ def run_rank(args):
                 extras = dict(EXTRAS_PARTIAL)
                 extras["error"] = f"{type(e).__name__}: {e}"[:500]
         else:
+            EXTRAS_PARTIAL["torch_nccl"] = {"skipped": "CPU rehearsal (PDCC_BENCH_DEVICE=cpu): no GPU"}
             extras = dict(EXTRAS_PARTIAL)
         timer.cancel()
+    TIMING["total"] = round(time.time() - T_START, 3)
     emit(extras)
     guard = threading.Timer(60.0, lambda: os._exit(0))  # teardown must not hang the job either
     guard.daemon = True
     guard.start()
     dist.destroy_process_group()
+
+
+def rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args):
+    """RCCL reads NCCL_BUFFSIZE / NCCL_PROTO once per process: measure them in fresh child
+    ranks before this rank touches the GPU (utils/rccl_env.py), and apply the winner to this
+    rank's own communicators (every rank applies the same one). Distinct GPUs only."""
+    if not on_gpu:
+        return {"skipped": "CPU rehearsal (PDCC_BENCH_DEVICE=cpu)"}
+    if world < 2:
+        return {"skipped": "world=1: no communicator to tune"}
+    if ngpu < world:
+        return {"skipped": f"ranks share a GPU ({world} ranks, {ngpu} GPU): RCCL refuses duplicate devices"}
+    if os.environ.get("PDCC_BENCH_RCCL_ENV_SWEEP", "1") == "0":
+        return {"skipped": "PDCC_BENCH_RCCL_ENV_SWEEP=0"}
+    if any(os.environ.get(k) for k in ("NCCL_BUFFSIZE", "NCCL_PROTO", "PDCC_RCCL_BUFFSIZE", "PDCC_RCCL_PROTO")):
+        return {"skipped": "NCCL_BUFFSIZE / NCCL_PROTO set by the user"}
+    from pytorch_distributed_collective_communication_amd.utils import rccl_env
+
+    if rank == 0:
+        print("[bench] RCCL environment pre-sweep (fresh child ranks per point)", file=sys.stderr, flush=True)
+    try:
+        rec, env = rccl_env.sweep(store, rank, world, local, nbytes=args.bytes if not SMALL else 64 << 20,
+                                  budget_s=float(os.environ.get("PDCC_BENCH_RCCL_ENV_SWEEP_S", "90")))
+    except Exception as e:  # never in the way of the headline
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    for k, v in env.items():
+        os.environ[k] = v  # before this process's first RCCL communicator
+    return rec
 
 
 def _time_op(fn, iters, warm=2):
@@ -320,8 +394,50 @@ def run_extras(world, rank, dev, native, x):
     from pytorch_distributed_collective_communication_amd import ops
 
     out = EXTRAS_PARTIAL  # filled in place, so a deadline still reports what finished
-    # K1 on this GPU: 2-source fp32 reduce of 256 MiB per source: LDS-DMA vs register staging,
-    # the non-temporal LDS-DMA default and the streaming kernel, and torch.add on the same data
+    with section("k1"):
+        run_k1(world, dev, out)
+    if world == 1:
+        out["torch_nccl"] = {"skipped": "world=1: all_reduce is a no-op"}
+        return out
+    out["links"] = link_summary(world)
+    # torch's own ProcessGroupNCCL over the same RCCL first: the bar this library must beat
+    with section("torch_nccl"):
+        try:
+            out["torch_nccl"] = torch_nccl_compare(world, rank, dev, native, x)
+        except Exception as e:
+            out["torch_nccl"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    with section("algo_ab"):
+        stopped = algo_ab(world, rank, dev, native, x, out)
+    if not stopped:
+        with section("baseline_configs"):
+            try:
+                out["baseline_configs"] = baseline_configs(world, rank, dev, x)
+            except Exception as e:
+                out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
+        if isinstance(out.get("torch_nccl"), dict) and isinstance(out.get("baseline_configs"), dict):
+            out["torch_nccl"]["vs_torch_nccl"] = vs_torch_nccl(out["baseline_configs"], out["torch_nccl"])
+        with section("graph_replay"):
+            out.update(graph_replay(world, rank, dev))
+        with section("rccl_tuning"):
+            try:
+                out["rccl_tuning"] = rccl_tuning(world, rank, dev, x)
+            except Exception as e:
+                out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
+        with section("ipc_grid_sweep"):
+            try:
+                out["ipc_grid_sweep_allreduce_busbw"] = ipc_grid_sweep(world, rank, dev, x)
+            except Exception as e:
+                out["ipc_grid_sweep_error"] = f"{type(e).__name__}: {e}"[:300]
+    return out
+
+
+def run_k1(world, dev, out):
+    """K1 on this GPU: 2-source fp32 reduce of 256 MiB per source: LDS-DMA vs register staging,
+    the non-temporal LDS-DMA default and the streaming kernel, and torch.add on the same data."""
+    import torch
+
+    from pytorch_distributed_collective_communication_amd import ops
+
     n = 64 << 20
     a = torch.rand(n, device=dev)
     b = torch.rand(n, device=dev)
@@ -337,9 +453,13 @@ def run_extras(world, rank, dev, native, x):
     ok = bool(torch.allclose(c, a + b))
     out["k1_correct"] = ok
     del a, b, c
-    if world == 1:
-        return out
-    out["links"] = link_summary(world)
+
+
+def algo_ab(world, rank, dev, native, x, out):
+    """Each engine forced in turn on the all_reduce sizes and three other collectives; returns
+    True if the ranks stopped after an engine that failed (the rest of the extras is skipped)."""
+    import torch
+    import torch.distributed as dist
 
     # algorithm A/B on a short-timeout subgroup (a stuck peer aborts in 60 s, not 10 min)
     g = dist.new_group(list(range(world)), timeout=datetime.timedelta(seconds=60))
@@ -408,21 +528,7 @@ def run_extras(world, rank, dev, native, x):
         gb.set_algo("auto")
     except Exception:
         pass
-    if "stopped_after" not in out:
-        try:
-            out["baseline_configs"] = baseline_configs(world, rank, dev, x)
-        except Exception as e:
-            out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
-        out.update(graph_replay(world, rank, dev))
-        try:
-            out["rccl_tuning"] = rccl_tuning(world, rank, dev, x)
-        except Exception as e:
-            out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
-        try:
-            out["ipc_grid_sweep_allreduce_busbw"] = ipc_grid_sweep(world, rank, dev, x)
-        except Exception as e:
-            out["ipc_grid_sweep_error"] = f"{type(e).__name__}: {e}"[:300]
-    return out
+    return "stopped_after" in out
 
 
 def link_summary(world):
@@ -614,67 +720,104 @@ def _p50_coll(fn, iters=5):
 _p50_coll.group = None  # the group whose engine _p50_coll reports (None: default group)
 
 
-def baseline_configs(world, rank, dev, x):
+def baseline_configs(world, rank, dev, x, group=None, engine=None):
     """The other BASELINE.json configs on this node (default algorithm selection):
     six collectives at S = 1 GiB fp32, PRODUCT/MAX/MIN all_reduce at 128 MiB,
-    all_gather bf16 4 GiB/rank (ZeRO-style), all_reduce 256 MiB at w=2."""
+    all_gather bf16 4 GiB/rank (ZeRO-style), all_reduce 256 MiB at w=2.
+    `group` / `engine`: the same rows on another group (torch's ProcessGroupNCCL)."""
     import torch
     import torch.distributed as dist
 
     from pytorch_distributed_collective_communication_amd.utils import busbw as bb
 
     res = {}
+    g = group
+    _p50_coll.group = group if engine is None else None
 
     def rec(name, coll, total_bytes, fn, iters=5, check=None):
-        progress(name)
+        progress(name if engine is None else f"{engine}: {name}")
         t = _p50_coll(fn, iters)
         res[name] = {"p50_ms": round(t * 1e3, 3), "busbw_GBps": round(bb(coll, total_bytes, world, t), 1),
-                     "engine": _p50_coll.engine}
+                     "engine": engine or _p50_coll.engine}
         if check is not None:
             res[name]["correct"] = bool(check())
 
-    S = 1 << 30 if not SMALL else 64 << 20
-    n = S // 4
-    chunk = n // world
-    x.uniform_(0.0, 1e-3)
-    rec("all_reduce_1GiB", "all_reduce", S, lambda: dist.all_reduce(x))
-    rec("reduce_1GiB", "reduce", S, lambda: dist.reduce(x, dst=0))
-    rec("broadcast_1GiB", "broadcast", S, lambda: dist.broadcast(x, src=0))
-    src = torch.full((chunk,), float(rank), device=dev)
-    out = torch.empty(n - n % world, device=dev)
-    rec("all_gather_1GiB", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src),
-        check=lambda: torch.equal(out.view(world, chunk)[:, 0].cpu(), torch.arange(world, dtype=torch.float32)))
-    glist = [torch.empty(chunk, device=dev) for _ in range(world)] if rank == 0 else None
-    rec("gather_1GiB", "gather", S, lambda: dist.gather(src, gather_list=glist, dst=0),
-        check=lambda: rank != 0 or all(bool(glist[r][0].item() == r) for r in range(world)))
-    slist = [torch.full((chunk,), float(r), device=dev) for r in range(world)] if rank == 0 else None
-    sout = torch.empty(chunk, device=dev)
-    rec("scatter_1GiB", "scatter", S, lambda: dist.scatter(sout, scatter_list=slist, src=0),
-        check=lambda: sout[0].item() == rank)
-    del glist, slist
-    rsin = torch.ones(n - n % world, device=dev)
-    rec("reduce_scatter_1GiB", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin),
-        check=lambda: sout[0].item() == world)
-    a2a = torch.empty_like(rsin)
-    rec("all_to_all_1GiB", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin))
-    del rsin, a2a, out, src
-    m = ((128 << 20) if not SMALL else (8 << 20)) // 4
-    for op in ("PRODUCT", "MAX", "MIN"):
-        v = torch.full((m,), 1.0 + 1e-7 * rank, device=dev)
-        rec(f"all_reduce_{op}_128MiB", "all_reduce", 128 << 20,
-            lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op)))
-    del v
-    if world == 2:
-        rec("all_reduce_256MiB", "all_reduce", 256 << 20, lambda: dist.all_reduce(x[: (256 << 20) // 4]))
-    per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
-    ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)
-    ag_out = torch.empty(per * world, dtype=torch.bfloat16, device=dev)
-    rec("all_gather_bf16_4GiB_per_rank", "all_gather", per * 2 * world,
-        lambda: dist.all_gather_into_tensor(ag_out, ag_in), iters=3,
-        check=lambda: torch.equal(ag_out.view(world, per)[:, -1].float().cpu(), torch.arange(world, dtype=torch.float32)))
-    del ag_in, ag_out
-    torch.cuda.empty_cache()
+    try:
+        S = 1 << 30 if not SMALL else 64 << 20
+        n = S // 4
+        chunk = n // world
+        x.uniform_(0.0, 1e-3)
+        rec("all_reduce_1GiB", "all_reduce", S, lambda: dist.all_reduce(x, group=g))
+        rec("reduce_1GiB", "reduce", S, lambda: dist.reduce(x, dst=0, group=g))
+        rec("broadcast_1GiB", "broadcast", S, lambda: dist.broadcast(x, src=0, group=g))
+        src = torch.full((chunk,), float(rank), device=dev)
+        out = torch.empty(n - n % world, device=dev)
+        rec("all_gather_1GiB", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src, group=g),
+            check=lambda: torch.equal(out.view(world, chunk)[:, 0].cpu(), torch.arange(world, dtype=torch.float32)))
+        glist = [torch.empty(chunk, device=dev) for _ in range(world)] if rank == 0 else None
+        rec("gather_1GiB", "gather", S, lambda: dist.gather(src, gather_list=glist, dst=0, group=g),
+            check=lambda: rank != 0 or all(bool(glist[r][0].item() == r) for r in range(world)))
+        slist = [torch.full((chunk,), float(r), device=dev) for r in range(world)] if rank == 0 else None
+        sout = torch.empty(chunk, device=dev)
+        rec("scatter_1GiB", "scatter", S, lambda: dist.scatter(sout, scatter_list=slist, src=0, group=g),
+            check=lambda: sout[0].item() == rank)
+        del glist, slist
+        rsin = torch.ones(n - n % world, device=dev)
+        rec("reduce_scatter_1GiB", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin, group=g),
+            check=lambda: sout[0].item() == world)
+        a2a = torch.empty_like(rsin)
+        rec("all_to_all_1GiB", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin, group=g))
+        del rsin, a2a, out, src
+        m = ((128 << 20) if not SMALL else (8 << 20)) // 4
+        for op in ("PRODUCT", "MAX", "MIN"):
+            v = torch.full((m,), 1.0 + 1e-7 * rank, device=dev)
+            rec(f"all_reduce_{op}_128MiB", "all_reduce", m * 4,
+                lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op), group=g))
+        del v
+        if world == 2:
+            rec("all_reduce_256MiB", "all_reduce", 256 << 20, lambda: dist.all_reduce(x[: (256 << 20) // 4], group=g))
+        per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
+        ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)
+        ag_out = torch.empty(per * world, dtype=torch.bfloat16, device=dev)
+        rec("all_gather_bf16_4GiB_per_rank", "all_gather", per * 2 * world,
+            lambda: dist.all_gather_into_tensor(ag_out, ag_in, group=g), iters=3,
+            check=lambda: torch.equal(ag_out.view(world, per)[:, -1].float().cpu(),
+                                      torch.arange(world, dtype=torch.float32)))
+        del ag_in, ag_out
+    finally:
+        _p50_coll.group = None
+        torch.cuda.empty_cache()
     return res
+
+
+def torch_nccl_compare(world, rank, dev, native, x):
+    """The bar the library has to clear: torch's own ProcessGroupNCCL (``backend="nccl"``, the
+    stock RCCL ProcessGroup the reference's dist.* calls would reach on GPU tensors,
+    main.py:5,94) on the same tensors and the same rows as baseline_configs: the 1 GiB
+    all_reduce headline, the six 1 GiB collectives, PRODUCT/MAX/MIN at 128 MiB, the bf16
+    ZeRO gather. vs_torch_nccl (added by run_extras) = torch's p50 / ours per row (> 1: ours
+    is faster)."""
+    import torch.distributed as dist
+
+    if "rccl_ok=1" not in native.describe():
+        return {"skipped": "ranks share a GPU: RCCL (and so ProcessGroupNCCL) refuses duplicate devices"}
+    progress("torch ProcessGroupNCCL comparator")
+    g = dist.new_group(list(range(world)), backend="nccl", timeout=datetime.timedelta(seconds=120))
+    try:
+        rows = baseline_configs(world, rank, dev, x, group=g, engine="torch_nccl")
+    finally:
+        dist.destroy_process_group(g)
+    return {"rows": rows}
+
+
+def vs_torch_nccl(ours: dict, theirs: dict) -> dict:
+    rows = theirs.get("rows", {}) if isinstance(theirs, dict) else {}
+    out = {}
+    for k, v in rows.items():
+        o = ours.get(k)
+        if isinstance(o, dict) and o.get("p50_ms") and v.get("p50_ms"):
+            out[k] = round(v["p50_ms"] / o["p50_ms"], 3)
+    return out
 
 
 def _time_local(fn, iters):

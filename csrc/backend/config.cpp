@@ -1,6 +1,9 @@
 #include "config.h"
 
+#include "../kernels/kernel_api.h"
+
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <sstream>
 #include <stdexcept>
@@ -81,6 +84,13 @@ Config Config::from_env() {
   c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
   c.ipc_ll_max = env_size("PDCC_IPC_LL_MAX", c.ipc_ll_max);
   c.ipc_zc_cache = std::max<size_t>(1, env_size("PDCC_IPC_ZC_CACHE", c.ipc_zc_cache));
+  if (c.ipc_zc_cache > (size_t)kern::kZcTab) {
+    fprintf(stderr, "[pdcc] PDCC_IPC_ZC_CACHE=%zu exceeds the device mapping table (%d per peer): clamped\n",
+            c.ipc_zc_cache, kern::kZcTab);
+    c.ipc_zc_cache = (size_t)kern::kZcTab;
+  }
+  c.ipc_zx = env_bool("PDCC_IPC_ZX", c.ipc_zx);
+  c.ipc_async_grid = std::min(1024, std::max(0, env_int("PDCC_IPC_ASYNC_GRID", c.ipc_async_grid)));
   c.ipc_zc_async = env_bool("PDCC_IPC_ZC_ASYNC", c.ipc_zc_async);
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
   c.autotune_min = env_size("PDCC_AUTOTUNE_MIN", c.autotune_min);
@@ -129,6 +139,8 @@ Config Config::from_env() {
     else throw std::runtime_error("PDCC_LIST_GATHER must be p2p|staged, got " + v);
   }
   c.a2a_list_agree = env_bool("PDCC_A2A_LIST_AGREE", c.a2a_list_agree);
+  if (const char* it = env("PDCC_RCCL_INIT_TIMEOUT_S")) c.rccl_init_timeout_ms = (int64_t)(std::atof(it) * 1000.0);
+  c.rccl_init_timeout_ms = std::max<int64_t>(1, c.rccl_init_timeout_ms);
   c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
   c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
   c.rccl_wide_ctas = std::max(0, env_int("PDCC_RCCL_WIDE_CTAS", c.rccl_wide_ctas));
@@ -164,9 +176,9 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
-    << " rccl_wide_min=" << rccl_wide_min
+    << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
     << " a2a_list_agree=" << a2a_list_agree

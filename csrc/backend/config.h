@@ -47,7 +47,17 @@ struct Config {
   // (256 KiB: LL beats the staged protocols at 128-256 KiB on MI355X, 8.1 vs 14.9 us per 256 KiB
   // all_reduce at W = 2, 11.6 vs 23.7 at W = 4: profiles/r3/ll_bench_256k_r3.jsonl)
   size_t ipc_ll_max = 256u << 10;          // PDCC_IPC_LL_MAX
+  // (at most kern::kZcTab: the device-side exchange looks mappings up in a table of that many
+  // entries per peer; a larger cache would silently send calls to the host gate)
   size_t ipc_zc_cache = 16;                // PDCC_IPC_ZC_CACHE
+  // Device-side record exchange of gated zero-copy calls (kern::ZcTable). Every rank's intent
+  // is voted on at the group's first GPU use (AND), so ranks with different settings agree.
+  bool ipc_zx = true;                      // PDCC_IPC_ZX
+  // Workgroup cap of IPC / LL launches issued on the comm stream (async_op=True collectives,
+  // e.g. DDP / ZeRO buckets overlapped with backward): the kernels spin in cross-GPU
+  // barriers while a peer lags, holding CU slots that the overlapped GEMMs need. 0 = no cap
+  // (the synchronous cap PDCC_IPC_GRID applies).
+  int ipc_async_grid = 0;                  // PDCC_IPC_ASYNC_GRID
   // Zero-copy calls exchange their records on a per-device launcher thread (IpcLauncher in
   // process_group.h): the caller's host never waits for its peers (0 = inline exchange)
   bool ipc_zc_async = true;                // PDCC_IPC_ZC_ASYNC
@@ -96,6 +106,11 @@ struct Config {
   // RCCL channel tuning: each CTA drives one channel (ring/tree lane); on 8 GPUs one
   // channel per xGMI link needs >= 7. -1 leaves RCCL's own topology tuner in charge
   // (ncclCommInitRank); any value set goes through ncclCommInitRankConfig.
+  // Deadline of one RCCL communicator creation (group comm, split / wide children, pair
+  // channels; capped by the group timeout): communicators are created non-blocking and
+  // polled, so a peer that dies or never arrives fails the group within this bound
+  // instead of hanging every other rank (the reference's Gloo surfaces it in ~0.2 s).
+  int64_t rccl_init_timeout_ms = 300000;   // PDCC_RCCL_INIT_TIMEOUT_S (seconds)
   int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
   int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
   // Wide RCCL: a child communicator (ncclCommSplit, own resources) with at least this many

@@ -13,846 +13,11 @@
 // Which one: a static size threshold (config.h) until the online autotuner has
 // timed both feasible engines for the call's (collective, dtype, op, size
 // bucket) on this very node; from then on the measured winner.
-#include <ATen/hip/HIPContext.h>
-#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
-#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
-
-#include <sys/file.h>
-#include <unistd.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstring>
-#include <sstream>
-#include <thread>
-
-#include "../device/comm_util.h"
-#include "process_group.h"
+#include "gpu_util.h"
 
 namespace pdcc {
 
-namespace {
-
-using RedOpType = c10d::ReduceOp::RedOpType;
-
-bool kern_dtype(at::ScalarType t, kern::DType& d) {
-  switch (t) {
-    case at::kFloat: d = kern::DType::F32; return true;
-    case at::kHalf: d = kern::DType::F16; return true;
-    case at::kBFloat16: d = kern::DType::BF16; return true;
-    case at::kDouble: d = kern::DType::F64; return true;
-    case at::kChar: d = kern::DType::I8; return true;
-    case at::kByte: d = kern::DType::U8; return true;
-    case at::kInt: d = kern::DType::I32; return true;
-    case at::kLong: d = kern::DType::I64; return true;
-    case at::kBool: d = kern::DType::BOOL; return true;
-    default: return false;
-  }
-}
-
-bool kern_op(RedOpType op, kern::RedOp& o) {
-  switch (op) {
-    case RedOpType::SUM: o = kern::RedOp::SUM; return true;
-    case RedOpType::AVG: o = kern::RedOp::AVG; return true;
-    case RedOpType::PRODUCT: o = kern::RedOp::PROD; return true;
-    case RedOpType::MIN: o = kern::RedOp::MIN; return true;
-    case RedOpType::MAX: o = kern::RedOp::MAX; return true;
-    case RedOpType::BAND: o = kern::RedOp::BAND; return true;
-    case RedOpType::BOR: o = kern::RedOp::BOR; return true;
-    case RedOpType::BXOR: o = kern::RedOp::BXOR; return true;
-    default: return false;
-  }
-}
-
-bool nccl_dtype(at::ScalarType t, ncclDataType_t& d) {
-  switch (t) {
-    case at::kFloat: d = ncclFloat32; return true;
-    case at::kHalf: d = ncclFloat16; return true;
-    case at::kBFloat16: d = ncclBfloat16; return true;
-    case at::kDouble: d = ncclFloat64; return true;
-    case at::kChar: d = ncclInt8; return true;
-    case at::kByte: d = ncclUint8; return true;
-    case at::kBool: d = ncclUint8; return true;
-    case at::kInt: d = ncclInt32; return true;
-    case at::kLong: d = ncclInt64; return true;
-    default: return false;
-  }
-}
-
-bool nccl_op(RedOpType op, at::ScalarType t, ncclRedOp_t& o) {
-  const bool b = t == at::kBool;  // bool: SUM = OR = max, PRODUCT = AND = min
-  switch (op) {
-    case RedOpType::SUM: o = b ? ncclMax : ncclSum; return true;
-    case RedOpType::PRODUCT: o = b ? ncclMin : ncclProd; return true;
-    case RedOpType::MIN: o = ncclMin; return true;
-    case RedOpType::MAX: o = ncclMax; return true;
-    case RedOpType::AVG: o = ncclAvg; return !b;
-    default: return false;  // BAND/BOR/BXOR: no RCCL op (IPC kernels or the host path)
-  }
-}
-
-const char* op_name(int op) {
-  switch (op) {
-    case RedOpType::SUM: return "SUM";
-    case RedOpType::AVG: return "AVG";
-    case RedOpType::PRODUCT: return "PRODUCT";
-    case RedOpType::MIN: return "MIN";
-    case RedOpType::MAX: return "MAX";
-    case RedOpType::BAND: return "BAND";
-    case RedOpType::BOR: return "BOR";
-    case RedOpType::BXOR: return "BXOR";
-    default: return "?";
-  }
-}
-
-// tune-key "op" slot of the copy collectives: the output/input list layout
-constexpr int kLayoutFlat = 100, kLayoutList = 101;
-
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
-
-// input used in place: contiguous + 16-B aligned, else a copy (on the current stream)
-at::Tensor prep_in(const at::Tensor& t) {
-  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
-  at::Tensor c = at::empty_like(t, at::MemoryFormat::Contiguous);
-  c.copy_(t);
-  return c;
-}
-// pure output: contiguous + aligned, else fresh storage (copied back afterwards)
-at::Tensor prep_out(const at::Tensor& t) {
-  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
-  return at::empty_like(t, at::MemoryFormat::Contiguous);
-}
-
-// consecutive views of one allocation, in rank order?
-bool is_flat(const std::vector<at::Tensor>& v, size_t bytes) {
-  if (v.empty()) return false;
-  const char* base = static_cast<const char*>(v[0].data_ptr());
-  for (size_t i = 0; i < v.size(); ++i) {
-    if (!v[i].is_contiguous()) return false;
-    if (static_cast<const char*>(v[i].data_ptr()) != base + i * bytes) return false;
-  }
-  return true;
-}
-
-// K2 (one launch) when every descriptor is 16-B aligned, hipMemcpyAsync otherwise
-void multi_copy_or_memcpy(const std::vector<kern::CopyDesc>& d, hipStream_t s) {
-  bool ok = true;
-  for (const auto& x : d) ok = ok && aligned16(x.src) && aligned16(x.dst);
-  if (ok) {
-    PDCC_HIP(kern::multi_copy(d.data(), (int)d.size(), s));
-  } else {
-    for (const auto& x : d)
-      if (x.bytes) PDCC_HIP(hipMemcpyAsync(x.dst, x.src, x.bytes, hipMemcpyDeviceToDevice, s));
-  }
-}
-
-int size_bucket(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned long long)bytes) : 0; }
-
-// is `s` being captured into a graph (torch.cuda.graph / parallel.graphs)?
-bool capturing(hipStream_t s) {
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
-}
-bool capturing_on(int device) {
-  return capturing(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device).stream());
-}
-hipStream_t current_stream(int device) {
-  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)device).stream();
-}
-
-// host path only competes for small messages, where its latency can beat a GPU protocol
-constexpr size_t kHostTuneMax = 4u << 20;
-
-// autotuner numerics check: candidate result vs the reference engine's result on the same data
-bool results_match(const at::Tensor& ref, const at::Tensor& got, RedOpType op, int world) {
-  if (!ref.is_floating_point() || op == RedOpType::MAX || op == RedOpType::MIN) return at::equal(ref, got);
-  const at::Tensor r = ref.to(at::kFloat), g = got.to(at::kFloat);
-  const bool wide = ref.scalar_type() == at::kFloat || ref.scalar_type() == at::kDouble;
-  // engines differ only in summation order (and, for 16-bit types, in where they round):
-  // allow a few ulps per rank relative to the largest magnitude; stale or misplaced data is far off
-  const double amax = r.abs().max().item<double>();
-  const double tol = (wide ? 4e-7 : 8e-3) * world;
-  if (!std::isfinite(amax)) return at::equal(ref, got);
-  return at::allclose(g, r, tol, tol * amax + 1e-30);
-}
-
-bool lists_equal(const std::vector<at::Tensor>& a, const std::vector<at::Tensor>& b) {
-  if (a.size() != b.size()) return false;
-  for (size_t i = 0; i < a.size(); ++i)
-    if (!at::equal(a[i], b[i])) return false;
-  return true;
-}
-
-// Elements of a tuning sample: at most `budget` bytes (per `units` tensors), a whole
-// number of 16-B vectors unless the full tensor fits.
-int64_t sample_numel(int64_t numel, size_t esize, size_t budget, int units = 1) {
-  const int64_t cap = (int64_t)(budget / std::max<size_t>(1, esize) / std::max(1, units));
-  if (numel <= cap) return numel;
-  const int64_t vec = std::max<int64_t>(1, 16 / (int64_t)esize);
-  return std::max<int64_t>(vec, cap / vec * vec);
-}
-
-// Read-only inputs for a tuning run: the first n elements of each tensor; a flat list
-// stays flat (copied into one allocation) so the timed path is the one the call takes.
-std::vector<at::Tensor> sample_inputs(const std::vector<at::Tensor>& v, int64_t n, bool flat) {
-  if (v.empty() || n >= v[0].numel()) return v;
-  std::vector<at::Tensor> out;
-  if (flat) {
-    at::Tensor buf = at::empty({(int64_t)v.size() * n}, v[0].options());
-    for (size_t i = 0; i < v.size(); ++i) {
-      out.push_back(buf.narrow(0, (int64_t)i * n, n));
-      out.back().copy_(v[i].reshape({-1}).narrow(0, 0, n));
-    }
-  } else {
-    for (const auto& t : v) out.push_back(t.reshape({-1}).narrow(0, 0, n));
-  }
-  return out;
-}
-// Scratch outputs for a tuning run, laid out like the caller's (flat or separate tensors).
-std::vector<at::Tensor> scratch_outputs(const at::TensorOptions& opt, size_t count, int64_t n, bool flat) {
-  std::vector<at::Tensor> out;
-  if (flat) {
-    at::Tensor buf = at::empty({(int64_t)count * n}, opt);
-    for (size_t i = 0; i < count; ++i) out.push_back(buf.narrow(0, (int64_t)i * n, n));
-  } else {
-    for (size_t i = 0; i < count; ++i) out.push_back(at::empty({n}, opt));
-  }
-  return out;
-}
-
-// Which groups may split from / share each other's RCCL communicator: same member set
-std::string members_key(const std::vector<int64_t>& global_ranks, int size) {
-  std::vector<int64_t> r = global_ranks;
-  if (r.empty())
-    for (int i = 0; i < size; ++i) r.push_back(i);
-  std::sort(r.begin(), r.end());
-  std::ostringstream o;
-  for (size_t i = 0; i < r.size(); ++i) o << (i ? "," : "") << r[i];
-  return o.str();
-}
-
-// IPC self-test verdicts of earlier groups with the same member set on the same devices:
-// the topology did not change, so later groups skip the test when every rank has one.
-// '0' = no IPC, '1' = staged IPC only, '2' = staged and zero-copy IPC.
-std::mutex g_verdict_mu;
-std::map<std::string, char> g_ipc_verdict;
-
-}  // namespace
-
-std::string ProcessGroupMI355X::make_members_key(const std::vector<int64_t>& global_ranks, int size) {
-  return members_key(global_ranks, size);
-}
-
-// =================================================================== device state
-DeviceState& ProcessGroupMI355X::dev_local(const at::Tensor& t) { return dev_local_idx(t.device().index()); }
-
-DeviceState& ProcessGroupMI355X::dev_local_idx(int d) {
-  std::lock_guard<std::mutex> lk(init_mu_);
-  auto it = devs_.find(d);
-  if (it != devs_.end()) return *it->second;
-  TORCH_CHECK(devs_.empty(), "pdcc: one GPU per rank per process group (got a tensor on cuda:", d,
-              " after using cuda:", devs_.begin()->first, ")");
-  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)d);
-  auto ds = std::make_unique<DeviceState>(
-      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/cfg_.stream_mode == 1, (c10::DeviceIndex)d));
-  ds->device = d;
-  (void)ds->sync->prealloc();  // signal words for stream hand-offs (see StreamSync::alloc)
-  // this rank's device record, for point-to-point peers (non-blocking: set only; a
-  // peer reads it after posting its own, so a ring of first ops cannot wait in a cycle)
-  store_->set("pdcc/devrec/" + std::to_string(rank_), [&] {
-    char bus[64] = {0};
-    PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
-    char host[256] = {0};
-    gethostname(host, sizeof(host) - 1);
-    const std::string rec = std::string(host) + "|" + bus;
-    return std::vector<uint8_t>(rec.begin(), rec.end());
-  }());
-  DeviceState& ref = *ds;
-  devs_[d] = std::move(ds);
-  return ref;
-}
-
-DeviceState& ProcessGroupMI355X::dev_state(const at::Tensor& t) {
-  DeviceState& ds = dev_local(t);
-  std::lock_guard<std::mutex> lk(init_mu_);
-  if (!ds.topo) init_topology(ds);
-  return ds;
-}
-
-// PDCC_EAGER_INIT=1: everything the first GPU collective would set up (topology,
-// IPC self-test, RCCL communicator) happens in init_process_group / new_group,
-// on the current device -- so the first collective is not the one paying for
-// it, and a graph can be captured right away.
-void ProcessGroupMI355X::eager_init(int device) {
-  DeviceState& ds = dev_local_idx(device);
-  {
-    std::lock_guard<std::mutex> lk(init_mu_);
-    if (!ds.topo) init_topology(ds);
-  }
-  if ((size_ > 1 || !cfg_.world1_local) && ds.rccl_ok) rccl(ds);
-}
-
-// Collective over the group (init_mu_ held): where is every rank, can RCCL run (one
-// rank per device) and can the IPC path run (same host, every peer reachable, and
-// the protocol self-test passes on this topology).
-void ProcessGroupMI355X::init_topology(DeviceState& ds) {
-  const int d = ds.device;
-  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)d);
-  char bus[64] = {0};
-  PDCC_HIP(hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, d));
-  char host[256] = {0};
-  gethostname(host, sizeof(host) - 1);
-  const std::string rec = std::string(host) + "|" + bus;
-  const std::string vkey = members_key_ + "@" + rec;
-  char cached = '?';
-  {
-    std::lock_guard<std::mutex> lk(g_verdict_mu);
-    auto it = g_ipc_verdict.find(vkey);
-    if (it != g_ipc_verdict.end()) cached = it->second;
-  }
-  const std::string mine = rec + "#" + cached;
-  const auto all = store_allgather(store_, "pdcc/dev", rank_, size_, std::vector<uint8_t>(mine.begin(), mine.end()));
-  std::vector<std::string> recs;
-  bool all_cached = true;
-  for (const auto& v : all) {
-    const std::string s(v.begin(), v.end());
-    const size_t h = s.rfind('#');
-    recs.push_back(s.substr(0, h));
-    const char c = h + 1 < s.size() ? s[h + 1] : '?';
-    all_cached = all_cached && c != '?' && c == cached;
-  }
-  bool shared = false;
-  for (int a = 0; a < size_; ++a)
-    for (int b = a + 1; b < size_; ++b) shared = shared || recs[a] == recs[b];
-  bool ok = cfg_.ipc_enable && same_host_ && size_ >= 2 && size_ <= kern::kMaxRanks;
-  for (int r = 0; r < size_ && ok; ++r) {
-    if (recs[r] == rec) continue;
-    const std::string pb = recs[r].substr(recs[r].find('|') + 1);
-    int idx = -1;
-    if (hipDeviceGetByPCIBusId(&idx, pb.c_str()) != hipSuccess) {
-      (void)hipGetLastError();
-      ok = false;
-      break;
-    }
-    int can = 0;
-    if (hipDeviceCanAccessPeer(&can, d, idx) != hipSuccess || !can) ok = false;
-  }
-  // every rank must agree (a rank that cannot see its peers vetoes the IPC path)
-  const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
-  for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
-
-  ds.recs = recs;
-  ds.shared_device = shared;
-  ds.rccl_ok = !shared;
-  if (!ok) {
-    ds.ipc_ok = false;
-  } else if (!cfg_.ipc_selftest) {
-    ds.ipc_ok = true;
-    ds.zc_ok = cfg_.ipc_zc;
-    ds.ll_ok = cfg_.ipc_ll_max > 0;
-  } else if (all_cached) {
-    ds.ipc_ok = cached != '0';  // an earlier group with these members tested this topology
-    ds.zc_ok = ((cached - '0') & 2) != 0;
-    ds.ll_ok = ((cached - '0') & 4) != 0;
-  } else {
-    ds.ipc_ok = ipc_selftest(ds);
-    std::lock_guard<std::mutex> lk(g_verdict_mu);
-    // bit 0: IPC, bit 1: zero-copy, bit 2: LL all-reduce
-    g_ipc_verdict[vkey] = !ds.ipc_ok ? '0' : (char)('1' + (ds.zc_ok ? 2 : 0) + (ds.ll_ok ? 4 : 0));
-  }
-  ds.topo = true;
-  if (cfg_.log_level >= 1)
-    fprintf(stderr, "[pdcc r%d] device %d (%s): rccl_ok=%d ipc_ok=%d zc_ok=%d ll_ok=%d shared_device=%d%s\n", rank_, d,
-            bus, (int)ds.rccl_ok, (int)ds.ipc_ok, (int)ds.zc_ok, (int)ds.ll_ok, (int)shared,
-            all_cached ? " (cached IPC verdict)" : "");
-}
-
-RcclOpts ProcessGroupMI355X::rccl_opts() const {
-  RcclOpts o;
-  o.min_ctas = cfg_.rccl_min_ctas;
-  o.max_ctas = cfg_.rccl_max_ctas;
-  o.split_share = cfg_.rccl_split_share ? 1 : 0;
-  return o;
-}
-
-// The group's RCCL communicator (lazy, collective over the group). A group whose
-// members equal those of a live communicator on this device (every demo of the
-// reference builds new_group(range(size)), main.py:11,21,31,46,63,75) splits
-// from it instead of bootstrapping a new one. All ranks vote first, so a rank
-// that has no such parent (or a different one) sends everyone down the fresh path.
-RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
-  if (ds.rccl) return *ds.rccl;
-  const auto t0 = std::chrono::steady_clock::now();
-  const std::string mk = members_key_ + "@" + std::to_string(ds.device);
-  std::shared_ptr<RcclComm> c;
-  const char* how = "init";
-  if (cfg_.group_comm != 2) {
-    auto parent = rccl_registry_get(mk);
-    const std::string tag = parent ? parent->tag : std::string();
-    const auto all = store_allgather(store_, "pdcc/rccl_parent", rank_, size_, std::vector<uint8_t>(tag.begin(), tag.end()));
-    bool agree = !tag.empty();
-    for (const auto& v : all) agree = agree && std::string(v.begin(), v.end()) == tag;
-    if (agree) {
-      if (cfg_.group_comm == 1) {
-        c = parent;
-        c->add_user();  // from now on its issue order is enforced across streams (RcclComm::enter)
-        how = "share";
-      } else {
-        c = std::make_shared<RcclComm>(*parent, rank_, rccl_opts());
-        c->tag = parent->tag;
-        how = "split";
-      }
-    }
-  }
-  if (!c) {
-    c = std::make_shared<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device, rccl_opts());
-    c->tag = group_name_ + "#" + mk;
-  }
-  rccl_registry_put(mk, c);
-  {
-    std::lock_guard<std::mutex> lk(init_mu_);
-    ds.rccl = c;
-  }
-  record_setup(std::string("rccl_comm/") + how, t0);
-  if (cfg_.log_level >= 1 && rank_ == 0)
-    fprintf(stderr, "[pdcc r0] group '%s': RCCL communicator (%s) in %.1f ms\n", group_name_.c_str(), how,
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-  return *ds.rccl;
-}
-
-// The wide child of the group's communicator (collective over the group: created by
-// decide() on every rank when a key races it, or by a forced PDCC_ALGO=rccl_wide).
-RcclComm& ProcessGroupMI355X::rccl_wide(DeviceState& ds) {
-  if (ds.rccl_wide) return *ds.rccl_wide;
-  RcclComm& base = rccl(ds);
-  const auto t0 = std::chrono::steady_clock::now();
-  RcclOpts o = rccl_opts();
-  o.min_ctas = std::max(cfg_.rccl_wide_ctas, 1);
-  o.max_ctas = std::max(o.max_ctas, o.min_ctas);
-  o.split_share = 0;  // its own channels and buffers
-  auto c = std::make_shared<RcclComm>(base, rank_, o);
-  c->tag = base.tag + "#wide";
-  {
-    std::lock_guard<std::mutex> lk(init_mu_);
-    ds.rccl_wide = c;
-  }
-  record_setup("rccl_comm/wide", t0);
-  return *ds.rccl_wide;
-}
-
-// The send/recv channel to `peer` (created on first use; its communicator is
-// built by the channel's own thread, see PairChan).
-std::shared_ptr<PairChan> ProcessGroupMI355X::pair_chan(DeviceState& ds, int peer) {
-  std::lock_guard<std::mutex> lk(init_mu_);
-  auto it = ds.pairs.find(peer);
-  if (it != ds.pairs.end()) return it->second;
-  auto pc = std::make_shared<PairChan>(
-      c10::hip::getStreamFromPoolMasqueradingAsCUDA(/*isHighPriority=*/false, (c10::DeviceIndex)ds.device));
-  ds.pairs[peer] = pc;
-  return pc;
-}
-
-// Are this rank and `peer` on different GPUs of one host? From the group topology when a
-// collective already exchanged it, else from the peer's device record (posted by its
-// first GPU op in this group, before it waits on anybody).
-bool ProcessGroupMI355X::pair_on_distinct_devices(DeviceState& ds, int peer) {
-  {
-    std::lock_guard<std::mutex> lk(init_mu_);
-    if (ds.topo) return ds.recs[peer] != ds.recs[rank_];
-    auto it = ds.pair_distinct.find(peer);
-    if (it != ds.pair_distinct.end()) return it->second;
-  }
-  const auto mine = store_->get("pdcc/devrec/" + std::to_string(rank_));
-  const auto theirs = store_->get("pdcc/devrec/" + std::to_string(peer));
-  const std::string a(mine.begin(), mine.end()), b(theirs.begin(), theirs.end());
-  const bool distinct = a.substr(0, a.find('|')) == b.substr(0, b.find('|')) && a != b;
-  std::lock_guard<std::mutex> lk(init_mu_);
-  ds.pair_distinct[peer] = distinct;
-  return distinct;
-}
-
-IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
-  if (!ds.ipc) {
-    const uint64_t spin = (uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count()));
-    auto c = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging, spin,
-                                       ds.shared_device, cfg_.ipc_zc_cache);
-    c->set_grid_max(cfg_.ipc_grid);
-    std::lock_guard<std::mutex> lk(init_mu_);
-    ds.ipc = c;
-  }
-  return *ds.ipc;
-}
-
-// PDCC_IPC_SELFTEST (default on): before a group's first GPU collective, every
-// rank runs the IPC protocol once on known data -- 1-shot all-reduce, 2-shot
-// all-reduce over rows of W tiles with a partial last row and a ragged tail, and
-// an all-gather -- with a short spin timeout. Two store votes decide (after the
-// communicator is built, after the checks): one failure on any rank (handle
-// export or mapping, spin timeout, wrong data) turns IPC off for the whole group,
-// so a topology the protocol does not work on falls back to RCCL (or the host
-// path) instead of hanging or corrupting data. Called from init_topology() with
-// init_mu_ held, on the group's comm stream (never a capturing one).
-bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
-  auto vote = [&](const std::string& key, bool mine) {
-    const auto v = store_allgather(store_, key, rank_, size_, std::vector<uint8_t>{(uint8_t)mine});
-    bool all = true;
-    for (const auto& x : v) all = all && !x.empty() && x[0] == 1;
-    return all;
-  };
-  const int64_t spin_ms = std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_selftest_ms, timeout_.count()));
-  std::string why;
-  bool ok = true;
-  try {
-    ds.ipc = std::make_shared<IpcComm>(store_, "pdcc/ipc", rank_, size_, ds.device, cfg_.ipc_max_staging,
-                                       (uint64_t)spin_ms, ds.shared_device, cfg_.ipc_zc_cache);
-  } catch (const std::exception& e) {
-    ok = false;
-    why = e.what();
-  }
-  bool all = vote("pdcc/ipc_selftest/built", ok);
-  if (all) {
-    try {
-      IpcComm& ic = *ds.ipc;
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
-      const hipStream_t s = ds.stream.stream();
-      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-      const double tri = size_ * (size_ + 1) / 2.0;
-      for (const int64_t n : {int64_t{1000}, int64_t{3} * size_ * 1024 + 257}) {
-        const at::Tensor base = at::arange(n, opt).remainder(7);
-        at::Tensor x = base + (double)(rank_ + 1);
-        kern::IpcCall c{};
-        c.coll = n == 1000 ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT;
-        c.dtype = kern::DType::F32;
-        c.op = kern::RedOp::SUM;
-        c.avg_div = size_;
-        c.bytes = x.nbytes();
-        c.in[0] = x.data_ptr();
-        c.out[0] = x.data_ptr();
-        ic.launch(c, s);
-        ok = at::equal(x, base * (double)size_ + tri) && ok;
-      }
-      const int64_t m = 780;  // 3120 B per rank: whole 16-B vectors, one partial tile
-      const at::Tensor in = at::full({m}, (double)rank_, opt);
-      at::Tensor out = at::full({m * size_}, -1.0, opt);
-      kern::IpcCall c{};
-      c.coll = kern::IpcColl::ALLGATHER;
-      c.dtype = kern::DType::U8;
-      c.op = kern::RedOp::COPY;
-      c.bytes = in.nbytes();
-      c.in[0] = in.data_ptr();
-      for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
-      ic.launch(c, s);
-      ok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && ok;
-      if (ic.error_word() != 0) {
-        ok = false;
-        why = "a cross-GPU barrier timed out";
-      } else if (!ok) {
-        why = "wrong data";
-      }
-    } catch (const std::exception& e) {
-      ok = false;
-      why = e.what();
-    }
-    if (const char* f = std::getenv("PDCC_IPC_SELFTEST_FAIL"))  // test hook: this rank reports a failure
-      if (*f && std::atoi(f) == rank_) {
-        ok = false;
-        why = "PDCC_IPC_SELFTEST_FAIL";
-      }
-    all = vote("pdcc/ipc_selftest/result", ok);
-  }
-  if (!all) {
-    fprintf(stderr, "[pdcc r%d] IPC self-test failed (%s): group '%s' runs without the peer-memory path\n", rank_,
-            ok ? "on another rank" : why.c_str(), group_name_.c_str());
-    ds.ipc.reset();  // every rank voted after its own kernels finished: nothing touches these buffers any more
-    return false;
-  }
-  // zero-copy IPC (user buffers mapped per call and read in place): whole rows /
-  // tiles zero-copy plus a staged rest, twice on one buffer (first and cached
-  // mapping), all-gather with a ragged tail, reduce-scatter of a flat input
-  ds.zc_ok = false;
-  if (cfg_.ipc_zc) {
-    bool zok = true;
-    std::string zwhy;
-    IpcComm& ic = *ds.ipc;
-    try {
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
-      const hipStream_t s = ds.stream.stream();
-      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-      const int64_t tile_f = kern::kTileBytes / 4;
-      const int64_t n = 3 * size_ * tile_f + 257;
-      const at::Tensor base = at::arange(n, opt).remainder(5);
-      at::Tensor x = base + (double)(rank_ + 1);
-      const double tri = size_ * (size_ + 1) / 2.0;
-      for (int k = 0; k < 2; ++k) {
-        kern::IpcCall c{};
-        c.coll = kern::IpcColl::ALLREDUCE_2SHOT;
-        c.dtype = kern::DType::F32;
-        c.op = kern::RedOp::SUM;
-        c.avg_div = size_;
-        c.bytes = x.nbytes();
-        c.in[0] = x.data_ptr();
-        c.out[0] = x.data_ptr();
-        ipc_run(ds, c, x.data_ptr(), x.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s,
-                k == 0 ? "pdcc/ipc_selftest/zc_ar0" : "pdcc/ipc_selftest/zc_ar1");
-        const at::Tensor want = k == 0 ? base * (double)size_ + tri : (base * (double)size_ + tri) * (double)size_;
-        zok = at::equal(x, want) && zok;
-      }
-      const int64_t m = 2 * tile_f + 5;
-      const at::Tensor in = at::full({m}, (double)rank_, opt);
-      at::Tensor out = at::full({m * size_}, -1.0, opt);
-      {
-        kern::IpcCall c{};
-        c.coll = kern::IpcColl::ALLGATHER;
-        c.dtype = kern::DType::U8;
-        c.op = kern::RedOp::COPY;
-        c.bytes = in.nbytes();
-        c.in[0] = in.data_ptr();
-        for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
-        ipc_run(ds, c, in.data_ptr(), in.nbytes(), kern::kTileBytes, ic.max_staging(), s, "pdcc/ipc_selftest/zc_ag");
-        zok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && zok;
-      }
-      {
-        const at::Tensor rin = at::arange(size_ * 2 * tile_f, opt).remainder(3) + (double)rank_;
-        at::Tensor rout = at::full({2 * tile_f}, -1.0, opt);
-        kern::IpcCall c{};
-        c.coll = kern::IpcColl::REDUCE_SCATTER;
-        c.dtype = kern::DType::F32;
-        c.op = kern::RedOp::SUM;
-        c.avg_div = size_;
-        c.bytes = rout.nbytes();
-        c.zstride = rout.nbytes();
-        for (int r = 0; r < size_; ++r) c.in[r] = static_cast<const char*>(rin.data_ptr()) + r * rout.nbytes();
-        c.out[0] = rout.data_ptr();
-        ipc_run(ds, c, rin.data_ptr(), rin.nbytes(), kern::kTileBytes, ic.max_staging(), s, "pdcc/ipc_selftest/zc_rs");
-        const at::Tensor mine = rin.narrow(0, rank_ * 2 * tile_f, 2 * tile_f) - (double)rank_;
-        zok = at::equal(rout, mine * (double)size_ + (size_ - 1) * size_ / 2.0) && zok;
-      }
-      PDCC_HIP(hipStreamSynchronize(s));
-      if (ic.error_word() != 0) {
-        zok = false;
-        zwhy = "a cross-GPU barrier timed out";
-        ic.clear_error();
-      } else if (!zok) {
-        zwhy = "wrong data";
-      }
-    } catch (const std::exception& e) {
-      zok = false;
-      zwhy = e.what();
-    }
-    if (const char* f = std::getenv("PDCC_IPC_ZC_SELFTEST_FAIL"))  // test hook: this rank reports a failure
-      if (*f && std::atoi(f) == rank_) {
-        zok = false;
-        zwhy = "PDCC_IPC_ZC_SELFTEST_FAIL";
-      }
-    ds.zc_ok = vote("pdcc/ipc_selftest/zc", zok);
-    if (!ds.zc_ok)
-      fprintf(stderr, "[pdcc r%d] zero-copy IPC self-test failed (%s): group '%s' stages every IPC call\n", rank_,
-              zok ? "on another rank" : zwhy.c_str(), group_name_.c_str());
-  }
-  // Device-side record exchange of gated zero-copy launches (design.md §3): a gated all-reduce
-  // on a buffer every rank has mapped now must resolve on the device -- its host gate is not
-  // opened unless the kernel is still running after a grace period (then: staged fallback,
-  // and the device exchange stays off for the group)
-  if (ds.zc_ok && ds.ipc->zx_on()) {
-    bool xok = true;
-    std::string xwhy;
-    IpcComm& ic = *ds.ipc;
-    try {
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
-      const hipStream_t s = ds.stream.stream();
-      const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-      const int64_t row = (int64_t)size_ * (kern::kTileBytes / 4);
-      const at::Tensor base = at::arange(4 * row, opt).remainder(7);
-      at::Tensor x = base + (double)rank_;
-      // map x everywhere first (inline exchange through the store, like the zc self-test)
-      kern::IpcCall c{};
-      c.coll = kern::IpcColl::ALLREDUCE_2SHOT;
-      c.dtype = kern::DType::F32;
-      c.op = kern::RedOp::SUM;
-      c.avg_div = size_;
-      c.bytes = x.nbytes();
-      c.in[0] = x.data_ptr();
-      c.out[0] = x.data_ptr();
-      ipc_run(ds, c, x.data_ptr(), x.nbytes(), (size_t)size_ * kern::kTileBytes, ic.max_staging(), s,
-              "pdcc/ipc_selftest/zx_map");
-      const IpcComm::ZcRec mine = ic.zc_export(x.data_ptr(), x.nbytes(), false);
-      const uint64_t t = ic.gate_reserve();
-      ic.launch_gated(c, t, 0, mine, x.data_ptr(), s);
-      auto ev = ic.gate_mark(t, s);
-      const uint64_t tag = ic.zx_last_tag();
-      const auto t0 = std::chrono::steady_clock::now();
-      while (hipEventQuery(ev->ev) == hipErrorNotReady &&
-             std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(std::max<int64_t>(2000, spin_ms / 4)))
-        std::this_thread::sleep_for(std::chrono::microseconds(200));
-      (void)hipGetLastError();
-      ic.gate_publish(t, false, {});  // (a kernel still waiting for the host gate runs staged now)
-      PDCC_HIP(hipStreamSynchronize(s));
-      const at::Tensor once = base * (double)size_ + size_ * (size_ - 1) / 2.0;  // after the mapping call
-      const bool data_ok = at::equal(x, once * (double)size_);
-      const uint32_t verdict = ic.zx_verdict(tag);
-      if (ic.error_word() != 0) {
-        xok = false;
-        xwhy = "the device exchange or a barrier timed out";
-        ic.clear_error();
-      } else if (verdict != 1u) {
-        xok = false;
-        xwhy = "the kernel did not resolve the buffers on the device (verdict " + std::to_string(verdict) + ")";
-      } else if (!data_ok) {
-        xok = false;
-        xwhy = "wrong data";
-      }
-    } catch (const std::exception& e) {
-      xok = false;
-      xwhy = e.what();
-    }
-    if (const char* f = std::getenv("PDCC_IPC_ZX_SELFTEST_FAIL"))  // test hook: this rank reports a failure
-      if (*f && std::atoi(f) == rank_) {
-        xok = false;
-        xwhy = "PDCC_IPC_ZX_SELFTEST_FAIL";
-      }
-    const bool zx = vote("pdcc/ipc_selftest/zx", xok);
-    ic.set_zx(zx);
-    if (!zx)
-      fprintf(stderr, "[pdcc r%d] device-side zero-copy exchange self-test failed (%s): group '%s' gates zero-copy "
-              "calls on the host\n", rank_, xok ? "on another rank" : xwhy.c_str(), group_name_.c_str());
-  }
-  // LL all-reduce: payloads with a partial last line and the largest one, each twice
-  // (both slot parities), bf16 and f32
-  ds.ll_ok = false;
-  if (cfg_.ipc_ll_max > 0) {
-    bool lok = true;
-    std::string lwhy;
-    IpcComm& ic = *ds.ipc;
-    try {
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(ds.stream);
-      const hipStream_t s = ds.stream.stream();
-      const double tri = size_ * (size_ + 1) / 2.0;
-      const int64_t full = (int64_t)(kern::kLLMaxBytes / 4);
-      for (const int64_t n : {int64_t{1}, int64_t{1001}, full, full}) {
-        for (const auto dt : {at::kFloat, at::kBFloat16}) {
-          const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(dt);
-          const int64_t ne = dt == at::kFloat ? n : std::max<int64_t>(1, n / 2 - 1);  // bf16: odd byte counts too
-          const at::Tensor base = at::arange(ne, opt).remainder(3);
-          at::Tensor x = base + (double)(rank_ + 1);
-          kern::IpcCall c{};
-          c.coll = kern::IpcColl::ALLREDUCE_LL;
-          c.dtype = dt == at::kFloat ? kern::DType::F32 : kern::DType::BF16;
-          c.op = kern::RedOp::SUM;
-          c.avg_div = size_;
-          c.bytes = x.nbytes();
-          c.in[0] = x.data_ptr();
-          c.out[0] = x.data_ptr();
-          ic.launch(c, s);
-          lok = at::equal(x, base * (double)size_ + tri) && lok;
-        }
-      }
-      for (const int64_t m : {int64_t{3}, full}) {  // all-gather: a partial line, the maximum
-        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-        const at::Tensor in = at::full({m}, (double)rank_, opt);
-        at::Tensor out = at::full({m * size_}, -1.0, opt);
-        kern::IpcCall c{};
-        c.coll = kern::IpcColl::ALLGATHER_LL;
-        c.dtype = kern::DType::U8;
-        c.op = kern::RedOp::COPY;
-        c.bytes = in.nbytes();
-        c.in[0] = in.data_ptr();
-        for (int r = 0; r < size_; ++r) c.out[r] = static_cast<char*>(out.data_ptr()) + r * in.nbytes();
-        ic.launch(c, s);
-        lok = at::equal(out, at::arange(size_, opt).repeat_interleave(m)) && lok;
-      }
-      // rooted kinds (tokens on the pairs without data), first and last rank as root, a partial line
-      for (const int root : {0, size_ - 1}) {
-        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-        const int64_t m = 1001;
-        const bool am_root = rank_ == root;
-        kern::IpcCall c{};
-        c.dtype = kern::DType::U8;
-        c.op = kern::RedOp::COPY;
-        c.root = root;
-        c.bytes = (size_t)m * 4;
-        at::Tensor b = at::full({m}, am_root ? 7.0 : -1.0, opt);  // broadcast
-        c.coll = kern::IpcColl::BROADCAST_LL;
-        c.in[0] = b.data_ptr();
-        c.out[0] = b.data_ptr();
-        ic.launch(c, s);
-        lok = at::equal(b, at::full({m}, 7.0, opt)) && lok;
-        const at::Tensor src = at::arange(size_ * m, opt).view({size_, m}).add((double)rank_);  // scatter
-        at::Tensor sc = at::full({m}, -1.0, opt);
-        c.coll = kern::IpcColl::SCATTER_LL;
-        for (int r = 0; r < size_; ++r) c.in[r] = am_root ? src[r].data_ptr() : nullptr;
-        c.out[0] = sc.data_ptr();
-        ic.launch(c, s);
-        lok = at::equal(sc, at::arange(m, opt).add((double)(rank_ * m + root))) && lok;
-        const at::Tensor gi = at::full({m}, (double)rank_, opt);  // gather
-        at::Tensor go = at::full({size_, m}, -1.0, opt);
-        c.coll = kern::IpcColl::GATHER_LL;
-        c.in[0] = gi.data_ptr();
-        for (int r = 0; r < size_; ++r) c.out[r] = am_root ? go[r].data_ptr() : nullptr;
-        ic.launch(c, s);
-        lok = (am_root ? at::equal(go, at::arange(size_, opt).view({size_, 1}).expand({size_, m}))
-                       : at::equal(go, at::full({size_, m}, -1.0, opt))) && lok;
-        const at::Tensor rb = at::arange(m, opt).remainder(5);  // reduce (non-root tensors untouched)
-        at::Tensor rx = rb + (double)(rank_ + 1);
-        c.coll = kern::IpcColl::REDUCE_LL;
-        c.dtype = kern::DType::F32;
-        c.op = kern::RedOp::SUM;
-        c.avg_div = size_;
-        c.in[0] = rx.data_ptr();
-        c.out[0] = rx.data_ptr();
-        ic.launch(c, s);
-        const double tri = size_ * (size_ + 1) / 2.0;
-        lok = at::equal(rx, am_root ? rb * (double)size_ + tri : rb + (double)(rank_ + 1)) && lok;
-      }
-      {  // reduce-scatter and all-to-all: chunk q to rank q (a partial line per chunk)
-        const auto opt = at::TensorOptions().device(at::kCUDA, ds.device).dtype(at::kFloat);
-        const int64_t m = 333;
-        const at::Tensor src = at::arange(size_, opt).view({size_, 1}).add((double)(100 * rank_)).expand({size_, m})
-                                   .contiguous();  // chunk q = 100 * rank + q
-        at::Tensor rs = at::full({m}, -1.0, opt);
-        at::Tensor a2a = at::full({size_, m}, -1.0, opt);
-        kern::IpcCall c{};
-        c.coll = kern::IpcColl::REDUCE_SCATTER_LL;
-        c.dtype = kern::DType::F32;
-        c.op = kern::RedOp::SUM;
-        c.avg_div = size_;
-        c.bytes = (size_t)m * 4;
-        for (int r = 0; r < size_; ++r) c.in[r] = src[r].data_ptr();
-        c.out[0] = rs.data_ptr();
-        ic.launch(c, s);
-        lok = at::equal(rs, at::full({m}, 100.0 * (tri - size_) + (double)(size_ * rank_), opt)) && lok;
-        c.coll = kern::IpcColl::ALLTOALL_LL;
-        c.dtype = kern::DType::U8;
-        c.op = kern::RedOp::COPY;
-        for (int r = 0; r < size_; ++r) c.out[r] = a2a[r].data_ptr();
-        ic.launch(c, s);
-        lok = at::equal(a2a, at::arange(size_, opt).mul(100.0).add((double)rank_).view({size_, 1}).expand({size_, m}))
-              && lok;
-      }
-      PDCC_HIP(hipStreamSynchronize(s));
-      if (ic.error_word() != 0) {
-        lok = false;
-        lwhy = "an LL poll timed out";
-        ic.clear_error();
-      } else if (!lok) {
-        lwhy = "wrong data";
-      }
-    } catch (const std::exception& e) {
-      lok = false;
-      lwhy = e.what();
-    }
-    if (const char* f = std::getenv("PDCC_IPC_LL_SELFTEST_FAIL"))  // test hook: this rank reports a failure
-      if (*f && std::atoi(f) == rank_) {
-        lok = false;
-        lwhy = "PDCC_IPC_LL_SELFTEST_FAIL";
-      }
-    ds.ll_ok = vote("pdcc/ipc_selftest/ll", lok);
-    if (!ds.ll_ok)
-      fprintf(stderr, "[pdcc r%d] LL all-reduce self-test failed (%s): group '%s' uses the 1-shot protocol\n", rank_,
-              lok ? "on another rank" : lwhy.c_str(), group_name_.c_str());
-  }
-  ds.ipc->set_timeout_ms((uint64_t)std::max<int64_t>(1, std::min<int64_t>(cfg_.ipc_spin_ms, timeout_.count())));
-  return true;
-}
+using namespace gpu;
 
 bool ProcessGroupMI355X::bytes_in_ll_range(size_t bytes) const {
   return bytes > 0 && bytes <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes);
@@ -1059,6 +224,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   if (rx) roctx_push_((std::string("pdcc:") + coll_name(c)).c_str());
   {
     c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(comm);  // temporaries + copy-backs run on the comm stream
+    // an async collective (comm stream) runs next to the caller's compute: its IPC launches
+    // take at most PDCC_IPC_ASYNC_GRID workgroups
+    IpcComm::AsyncScope as(ipcp.get(), comm != cur && !stream);
     fn(comm.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
@@ -1148,298 +316,6 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_issue(Coll c, DeviceState
   return w;
 }
 
-// =================================================================== autotuner
-std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool rccl_can, bool ipc_can,
-                                                      bool zc_can, bool ll_can) const {
-  std::vector<Algo> v;
-  if (!cfg_.autotune || cfg_.force_algo != Algo::AUTO || !ipc_can || !same_host_ || coalescing_) return v;
-  if ((int)c >= 32 || !(cfg_.autotune_colls & (1u << (int)c))) return v;
-  if (bytes < cfg_.autotune_min || bytes > cfg_.autotune_max) return v;
-  // LL sizes keep the static choice: a race there would time the LL kernel and then apply
-  // the verdict to the staged protocol the rest of the power-of-two bucket takes
-  if (ll_can && bytes_in_ll_range(bytes)) return v;
-  if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
-  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
-  else return {};
-  // RCCL with more channels than its topology tuner picks (large all_reduce keys)
-  if (c == Coll::ALLREDUCE && rccl_can && cfg_.rccl_wide_ctas > 0 && bytes >= cfg_.rccl_wide_min)
-    v.push_back(Algo::RCCL_WIDE);
-  v.push_back(Algo::IPC);
-  // the pull all-reduce with more workgroups (distinct GPUs: rccl_can; shared devices are
-  // capped for co-residency anyway)
-  if (c == Coll::ALLREDUCE && rccl_can && cfg_.ipc_wide_grid > cfg_.ipc_grid && bytes >= cfg_.rccl_wide_min)
-    v.push_back(Algo::IPC_WIDE);
-  // the same IPC protocols without zero copy (zero-copy sizes): measured, not assumed, where the
-  // staging copy beats the per-call record exchange
-  if (zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min) v.push_back(Algo::IPC_STAGED);
-  // the push all-reduce (zero-copy sizes): every remote access a write instead of a read
-  if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
-      bytes > cfg_.ipc_1shot_max)
-    v.push_back(Algo::IPC_PUSH);
-  return v;
-}
-
-Algo ProcessGroupMI355X::tuned(const TuneKey& k) {
-  std::lock_guard<std::mutex> lk(tune_mu_);
-  auto it = tune_.find(k);
-  return it == tune_.end() ? Algo::AUTO : it->second.algo;
-}
-
-// The engine for one call. A decision for this key is used only if that engine is a
-// candidate of this call too; everything here depends on group-wide facts only
-// (topology, dtype/op support, the consensus table), so every rank picks the same.
-Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can,
-                                bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
-  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok, ds.ll_ok);
-  if (cands.empty()) return a0;
-  const TuneKey key{(int)c, dtype, op, size_bucket(bytes)};
-  const Algo t = tuned(key);
-  const bool cap = capturing_on(ds.device);
-  if (t != Algo::AUTO) {
-    if (std::find(cands.begin(), cands.end(), t) == cands.end()) return a0;
-    if (t == Algo::HOST && cap) return Algo::IPC;  // tuned to the host engine, which cannot be captured
-    return t;
-  }
-  if (!cfg_.autotune_file.empty()) {  // a decision recorded by an earlier run (same topology)
-    const Algo f = file_decision(key, ds);
-    if (f != Algo::AUTO && std::find(cands.begin(), cands.end(), f) != cands.end() && !(f == Algo::HOST && cap)) {
-      TuneEntry te;
-      te.ref = cands[0];
-      te.valid = true;
-      te.algo = f;  // iters = 0: from the file
-      std::lock_guard<std::mutex> lk(tune_mu_);
-      tune_[key] = te;
-      return f;
-    }
-  }
-  if (cap) return a0;  // no timing runs inside a graph capture: static choice
-  // every engine of the race exists before the clock starts (communicator setup is not timed)
-  for (Algo a : cands) {
-    if (a == Algo::RCCL) rccl(ds);
-    if (a == Algo::RCCL_WIDE) rccl_wide(ds);
-    if (is_ipc(a)) ipc(ds);
-  }
-  // the race runs on the caller's stream: it must not overlap an async collective of this
-  // group still in flight on the comm stream (IPC kernels of one rank share the per-block
-  // counters, the staging buffer and the LL epoch word)
-  order_after_async(ds, current_stream(ds.device));
-  return tune(key, cands);
-}
-
-Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
-                                  const std::function<void(size_t)>& run,
-                                  const std::function<bool(size_t, size_t)>& same) {
-  c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
-  const hipStream_t s = current_stream(ds.device);
-  const size_t n = cands.size();
-  auto elapsed_us = [](hipEvent_t a, hipEvent_t b) {
-    float ms = 0.f;
-    PDCC_HIP(hipEventElapsedTime(&ms, a, b));
-    return 1e3 * (double)ms;
-  };
-  // IPC runs of the race get a short spin bound: a run that cannot complete here
-  // disqualifies IPC for this key (below) instead of hanging the group
-  struct Spin {
-    IpcComm* ic;
-    uint64_t saved;
-    std::atomic<bool>& flag;
-    Spin(IpcComm* c, uint64_t ms, std::atomic<bool>& f) : ic(c), saved(c ? c->timeout_ms() : 0), flag(f) {
-      flag.store(true);
-      if (ic) ic->set_timeout_ms(std::max<uint64_t>(1, std::min<uint64_t>(ms, saved)));
-    }
-    ~Spin() {
-      if (ic) ic->set_timeout_ms(saved);
-      flag.store(false);
-    }
-  };
-  bool has_ipc = false;
-  for (Algo a : cands) has_ipc = has_ipc || is_ipc(a);
-  Spin spin(has_ipc ? ds.ipc.get() : nullptr, (uint64_t)cfg_.autotune_spin_ms, tuning_);
-  // 0) warm-up: one run each (staging growth, first-touch), then check every result
-  //    against the reference engine's on identical data
-  for (size_t k = 0; k < n; ++k) {
-    if (is_ipc(cands[k]))
-      if (const char* d = std::getenv("PDCC_TEST_AUTOTUNE_DELAY"))  // test hook "rank:ms": a late peer
-        if (std::atoi(d) == rank_) {
-          PDCC_HIP(hipStreamSynchronize(s));
-          std::this_thread::sleep_for(std::chrono::milliseconds(std::atoi(std::strchr(d, ':') + 1)));
-        }
-    run(k);
-  }
-  PDCC_HIP(hipStreamSynchronize(s));
-  std::vector<double> v(2 * n, 0.0);  // [estimate_us x n, mismatch x n], MAX-reduced across ranks
-  const bool ipc_fault = has_ipc && ds.ipc && ds.ipc->error_word() != 0;
-  for (size_t k = 1; k < n; ++k)
-    v[n + k] = (is_ipc(cands[k]) && ipc_fault) ? 2.0 : (same(0, k) ? 0.0 : 1.0);
-  {  // agree on faults first (every rank's stream is drained: no IPC kernel is running)
-    std::vector<double> f(v.begin() + n, v.end());
-    shm().allreduce(f.data(), f.size(), at::kDouble, RedOpType::MAX, timeout_);
-    std::copy(f.begin(), f.end(), v.begin() + n);
-  }
-  std::vector<bool> live(n, true);
-  for (size_t k = 1; k < n; ++k)
-    if (v[n + k] >= 2.0) {
-      live[k] = false;  // an IPC barrier timed out on some rank: drop IPC from the race
-      if (ds.ipc) ds.ipc->clear_error();
-      fprintf(stderr, "[pdcc r%d] autotune %s %zu B: IPC run timed out (>%lld ms); using %s for this key\n", rank_,
-              coll_name((Coll)std::get<0>(key)), bytes, (long long)cfg_.autotune_spin_ms, algo_name(cands[0]));
-    }
-  const std::function<void(size_t)> run_live = [&](size_t k) {
-    if (live[k]) run(k);
-  };
-  // 1) one timed run each: sizes the measurement (same count on every rank: MAX-reduced inputs)
-  std::vector<hipEvent_t> e1(n + 1);
-  for (auto& e : e1) PDCC_HIP(hipEventCreate(&e));
-  PDCC_HIP(hipEventRecord(e1[0], s));
-  for (size_t k = 0; k < n; ++k) {
-    run_live(k);
-    PDCC_HIP(hipEventRecord(e1[k + 1], s));
-  }
-  PDCC_HIP(hipEventSynchronize(e1[n]));
-  for (size_t k = 0; k < n; ++k) v[k] = elapsed_us(e1[k], e1[k + 1]);
-  for (auto& e : e1) hipEventDestroy(e);
-  shm().allreduce(v.data(), v.size(), at::kDouble, RedOpType::MAX, timeout_);
-  double slow = 1.0;
-  for (size_t k = 0; k < n; ++k) slow = std::max(slow, v[k]);
-  const int iters = (int)std::max(3.0, std::min(25.0, std::ceil(30000.0 / slow)));
-  // 2) interleaved timed runs (ref, ipc, ref, ipc, ...): drift hits both engines alike
-  std::vector<hipEvent_t> ev(iters * n + 1);
-  for (auto& e : ev) PDCC_HIP(hipEventCreate(&e));
-  PDCC_HIP(hipEventRecord(ev[0], s));
-  for (int i = 0; i < iters; ++i)
-    for (size_t k = 0; k < n; ++k) {
-      run_live(k);
-      PDCC_HIP(hipEventRecord(ev[i * n + k + 1], s));
-    }
-  PDCC_HIP(hipEventSynchronize(ev[iters * n]));
-  std::vector<double> med(n);
-  for (size_t k = 0; k < n; ++k) {
-    std::vector<double> t;
-    for (int i = 0; i < iters; ++i) t.push_back(elapsed_us(ev[i * n + k], ev[i * n + k + 1]));
-    std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
-    med[k] = t[t.size() / 2];
-  }
-  for (auto& e : ev) hipEventDestroy(e);
-  // 3) every rank adopts the same engine: slowest rank's median, any rank's mismatch
-  shm().allreduce(med.data(), med.size(), at::kDouble, RedOpType::MAX, timeout_);
-  size_t best = 0;
-  for (size_t k = 1; k < n; ++k)
-    if (live[k] && v[n + k] == 0.0 && med[k] < med[best]) best = k;
-  TuneEntry te;
-  te.ref = cands[0];
-  te.iters = iters;
-  te.valid = true;
-  for (size_t k = 0; k < n; ++k) {
-    if (is_ipc(cands[k])) {
-      (cands[k] == Algo::IPC          ? te.ipc_us
-       : cands[k] == Algo::IPC_WIDE   ? te.ipc_wide_us
-       : cands[k] == Algo::IPC_STAGED ? te.staged_us
-                                      : te.push_us) = med[k];
-      te.valid = te.valid && v[n + k] == 0.0;
-    } else if (cands[k] == Algo::RCCL_WIDE) {
-      te.wide_us = med[k];
-      te.valid = te.valid && v[n + k] == 0.0;
-    } else {
-      te.rccl_us = med[k];  // the reference engine (RCCL, or the host transport without RCCL)
-    }
-  }
-  te.algo = cands[best];
-  {
-    std::lock_guard<std::mutex> lk(tune_mu_);
-    tune_[key] = te;
-  }
-  if (!cfg_.autotune_file.empty() && rank_ == 0 && te.valid) file_append(key, te, ds);
-  if (cfg_.log_level >= 1 && rank_ == 0)
-    fprintf(stderr,
-            "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us,"
-            " ipc_staged %.1f us%s (%d runs each) -> %s\n",
-            coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us,
-            te.ipc_wide_us, te.push_us, te.staged_us,
-            te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
-  return te.algo;
-}
-
-// ---- PDCC_AUTOTUNE_FILE: one line per decision,
-//   pdcc-tune v1 <signature> <coll> <dtype> <op> <size bucket> <engine> [# times]
-// The signature names what the verdict depends on: world size, distinct or shared GPUs,
-// the GPU architecture and the IPC grid cap.
-std::string ProcessGroupMI355X::tune_sig(const DeviceState& ds) const {
-  hipDeviceProp_t p{};
-  std::string arch = hipGetDeviceProperties(&p, ds.device) == hipSuccess ? std::string(p.gcnArchName) : "?";
-  arch = arch.substr(0, arch.find(':'));
-  std::ostringstream o;
-  o << "w" << size_ << "-" << (ds.shared_device ? "shared" : "distinct") << "-" << arch << "-g" << cfg_.ipc_grid;
-  return o.str();
-}
-
-Algo ProcessGroupMI355X::file_decision(const TuneKey& key, DeviceState& ds) {
-  if (!tune_file_read_) {
-    tune_file_read_ = true;
-    const std::string sig = tune_sig(ds);
-    if (FILE* f = std::fopen(cfg_.autotune_file.c_str(), "r")) {
-      char line[512];
-      while (std::fgets(line, sizeof(line), f)) {
-        char tag[16], ver[8], sg[128], eng[32];
-        int c, dt, op, b;
-        if (std::sscanf(line, "%15s %7s %127s %d %d %d %d %31s", tag, ver, sg, &c, &dt, &op, &b, eng) != 8) continue;
-        if (std::strcmp(tag, "pdcc-tune") != 0 || std::strcmp(ver, "v1") != 0 || sig != sg) continue;
-        const Algo a = algo_from_name(eng);
-        if (a != Algo::AUTO) tune_file_[TuneKey{c, dt, op, b}] = a;  // later lines win
-      }
-      std::fclose(f);
-    }
-  }
-  const auto it = tune_file_.find(key);
-  double v[2] = {it == tune_file_.end() ? 0.0 : (double)(int)it->second, 0.0};
-  v[1] = -v[0];
-  shm().allreduce(v, 2, at::kDouble, RedOpType::MAX, timeout_);  // max and -min: agree only if equal
-  return v[0] == -v[1] ? (Algo)(int)v[0] : Algo::AUTO;
-}
-
-void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, const DeviceState& ds) {
-  FILE* f = std::fopen(cfg_.autotune_file.c_str(), "a");
-  if (!f) {
-    fprintf(stderr, "[pdcc r%d] PDCC_AUTOTUNE_FILE %s: cannot append\n", rank_, cfg_.autotune_file.c_str());
-    return;
-  }
-  flock(fileno(f), LOCK_EX);
-  std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
-               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f\n",
-               tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
-               algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref), (size_t)1 << std::get<3>(key),
-               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us);
-  std::fflush(f);
-  flock(fileno(f), LOCK_UN);
-  std::fclose(f);
-}
-
-std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table() {
-  std::lock_guard<std::mutex> lk(tune_mu_);
-  std::vector<TuneRecord> out;
-  for (const auto& kv : tune_) {
-    const TuneEntry& e = kv.second;
-    const int dt = std::get<1>(kv.first), op = std::get<2>(kv.first), b = std::get<3>(kv.first);
-    TuneRecord r;
-    r.coll = coll_name((Coll)std::get<0>(kv.first));
-    r.dtype = dt < 0 ? "-" : c10::toString((at::ScalarType)dt);
-    r.op = op == kLayoutFlat ? "flat" : op == kLayoutList ? "list" : op < 0 ? "-" : op_name(op);
-    r.lo = 1ull << b;
-    r.hi = 2ull << b;
-    r.ref = algo_name(e.ref);
-    r.rccl_us = e.rccl_us;
-    r.ipc_us = e.ipc_us;
-    r.push_us = e.push_us;
-    r.ipc_wide_us = e.ipc_wide_us;
-    r.staged_us = e.staged_us;
-    r.wide_us = e.wide_us;
-    r.valid = e.valid;
-    r.algo = algo_name(e.algo);
-    r.iters = e.iters;
-    out.push_back(r);
-  }
-  return out;
-}
-
 // =================================================================== engines
 void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko,
                                            ncclDataType_t nd, ncclRedOp_t no, bool nok, RedOpType op, int root,
@@ -1474,8 +350,8 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     TORCH_CHECK(nok, "pdcc: RCCL has no reduction for ", op_name(op), " on ", w.scalar_type());
     RcclComm& rc = a == Algo::RCCL_WIDE ? rccl_wide(ds) : rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
-    if (rooted) PDCC_NCCL(ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
-    else PDCC_NCCL(ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
+    if (rooted) PDCC_NCCLC(rc.get(), ncclReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, root, rc.get(), s));
+    else PDCC_NCCLC(rc.get(), ncclAllReduce(w.data_ptr(), w.data_ptr(), w.numel(), nd, no, rc.get(), s));
   } else {  // HOST, synchronous
     PDCC_HIP(hipStreamSynchronize(s));
     at::Tensor h = w.cpu();
@@ -1511,7 +387,7 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
-    PDCC_NCCL(ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rc.get(), s));
+    PDCC_NCCLC(rc.get(), ncclBroadcast(w.data_ptr(), w.data_ptr(), bytes, ncclUint8, root, rc.get(), s));
   } else {
     PDCC_HIP(hipStreamSynchronize(s));
     at::Tensor h = w.cpu();
@@ -1547,11 +423,11 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
     RcclComm& rc = rccl(ds);
     RcclComm::Issue og(rc, s, capturing(s));
     if (!rooted && is_flat(wo, bytes)) {
-      PDCC_NCCL(ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc.get(), s));
+      PDCC_NCCLC(rc.get(), ncclAllGather(wi.data_ptr(), wo[0].data_ptr(), bytes, ncclUint8, rc.get(), s));
     } else if (!rooted && !cfg_.list_gather_p2p) {
       // staged: one ring all-gather into a staging buffer, then K2 unpacks into the list
       at::Tensor stg = at::empty({(int64_t)(bytes * size_)}, wi.options().dtype(at::kByte));
-      PDCC_NCCL(ncclAllGather(wi.data_ptr(), stg.data_ptr(), bytes, ncclUint8, rc.get(), s));
+      PDCC_NCCLC(rc.get(), ncclAllGather(wi.data_ptr(), stg.data_ptr(), bytes, ncclUint8, rc.get(), s));
       std::vector<kern::CopyDesc> d;
       for (int r = 0; r < size_; ++r)
         d.push_back({static_cast<char*>(stg.data_ptr()) + r * bytes, wo[r].data_ptr(), bytes});
@@ -1565,7 +441,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
         if (!rooted || r == root) PDCC_NCCL(ncclSend(wi.data_ptr(), bytes, ncclUint8, r, rc.get(), s));
         if (receiver) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), bytes, ncclUint8, r, rc.get(), s));
       }
-      PDCC_NCCL(ncclGroupEnd());
+      PDCC_NCCLC(rc.get(), ncclGroupEnd());
       if (receiver && bytes)
         PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi.data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
     }
@@ -1620,7 +496,7 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
     } else {
       PDCC_NCCL(ncclRecv(wo.data_ptr(), bytes, ncclUint8, root, rc.get(), s));
     }
-    PDCC_NCCL(ncclGroupEnd());
+    PDCC_NCCLC(rc.get(), ncclGroupEnd());
     if (rank_ == root && bytes)
       PDCC_HIP(hipMemcpyAsync(wo.data_ptr(), wi[root].data_ptr(), bytes, hipMemcpyDeviceToDevice, s));
   } else {
@@ -1679,7 +555,7 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
       src = stg.data_ptr();
     }
     RcclComm::Issue og(rc, s, capturing(s));
-    PDCC_NCCL(ncclReduceScatter(src, wo.data_ptr(), wo.numel(), nd, no, rc.get(), s));
+    PDCC_NCCLC(rc.get(), ncclReduceScatter(src, wo.data_ptr(), wo.numel(), nd, no, rc.get(), s));
   } else {
     PDCC_HIP(hipStreamSynchronize(s));
     std::vector<at::Tensor> hi;
@@ -1722,7 +598,7 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
     RcclComm::Issue og(rc, s, capturing(s));
     const size_t chunk = wi[0].nbytes();
     if (equal && is_flat(wi, chunk) && is_flat(wo, chunk)) {
-      PDCC_NCCL(ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc.get(), s));
+      PDCC_NCCLC(rc.get(), ncclAllToAll(wi[0].data_ptr(), wo[0].data_ptr(), chunk, ncclUint8, rc.get(), s));
     } else {
       PDCC_NCCL(ncclGroupStart());
       for (int r = 0; r < size_; ++r) {
@@ -1730,7 +606,7 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
         if (wi[r].nbytes()) PDCC_NCCL(ncclSend(wi[r].data_ptr(), wi[r].nbytes(), ncclUint8, r, rc.get(), s));
         if (wo[r].nbytes()) PDCC_NCCL(ncclRecv(wo[r].data_ptr(), wo[r].nbytes(), ncclUint8, r, rc.get(), s));
       }
-      PDCC_NCCL(ncclGroupEnd());
+      PDCC_NCCLC(rc.get(), ncclGroupEnd());
       if (wi[rank_].nbytes())
         PDCC_HIP(hipMemcpyAsync(wo[rank_].data_ptr(), wi[rank_].data_ptr(), wi[rank_].nbytes(),
                                 hipMemcpyDeviceToDevice, s));
@@ -1758,7 +634,8 @@ void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>&
 
 // =================================================================== all-reduce / reduce
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, RedOpType op, int root, bool rooted,
-                                                                 std::chrono::milliseconds to) {
+                                                                 std::chrono::milliseconds to,
+                                                                 std::shared_ptr<const Coalesced> co) {
   const Coll cname = rooted ? Coll::REDUCE : Coll::ALLREDUCE;
   TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
   const auto t0 = std::chrono::steady_clock::now();
@@ -1792,8 +669,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
   if (a == Algo::HOST) {
     enqueue_allreduce(Algo::HOST, w, kd, ko, nd, no, nok, op, root, rooted, ds, current_stream(ds.device), to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+    if (co) co->run(current_stream(ds.device));
     record(cname, "host", bytes, t0);
-    return cpu_done(cname, {t});
+    return cpu_done(cname, co ? co->members : std::vector<at::Tensor>{t});
   }
   std::shared_ptr<IpcComm> icp;
   if (is_ipc(a)) {
@@ -1801,9 +679,13 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     icp = ds.ipc;
   }
   const bool one_shot = bytes <= cfg_.ipc_1shot_max;
-  auto work = gpu_issue(cname, ds, a, {t, w}, {t}, to, [=, dsp = &ds, t = t](hipStream_t x) mutable {
+  std::vector<at::Tensor> keep{t, w};
+  if (co) keep.insert(keep.end(), co->members.begin(), co->members.end());
+  auto work = gpu_issue(cname, ds, a, keep, co ? co->members : std::vector<at::Tensor>{t}, to,
+                        [=, dsp = &ds, t = t](hipStream_t x) mutable {
     enqueue_allreduce(a, w, kd, ko, nd, no, nok, op, root, rooted, *dsp, x, to);
     if (!w.is_same(t) && (!rooted || rank_ == root)) t.copy_(w);
+    if (co) co->run(x);
   }, icp);
   const bool ll = ds.ll_ok && bytes_in_ll_range(bytes);
   record(cname, is_ipc(a) ? (ll                                 ? "ipc_ll"
@@ -1862,7 +744,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
 // =================================================================== all-gather / gather
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at::Tensor>& outs, at::Tensor& in,
                                                                  int root, bool rooted,
-                                                                 std::chrono::milliseconds to) {
+                                                                 std::chrono::milliseconds to,
+                                                                 std::shared_ptr<const Coalesced> co) {
   const Coll cname = rooted ? Coll::GATHER : Coll::ALLGATHER;
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = in.nbytes();
@@ -1898,11 +781,13 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     if (receiver)
       for (int r = 0; r < size_; ++r)
         if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+    if (co) co->run(current_stream(ds.device));
     record(cname, "host", bytes, t0);
-    return cpu_done(cname, outs);
+    return cpu_done(cname, co ? co->members : outs);
   }
   std::vector<at::Tensor> keep{in, wi};
   for (auto& o : wo) keep.push_back(o);
+  if (co) keep.insert(keep.end(), co->members.begin(), co->members.end());
   std::shared_ptr<IpcComm> icp;
   if (is_ipc(a)) {
     ipc(ds);
@@ -1911,11 +796,13 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
   const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
   const char* algo = is_ipc(a) ? (ll ? "ipc_ll" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
-  auto work = gpu_issue(cname, ds, a, keep, outs, to, [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
+  auto work = gpu_issue(cname, ds, a, keep, co ? co->members : outs, to,
+                        [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
     enqueue_allgather(a, wi, wo, root, rooted, *dsp, x, to);
     if (receiver)
       for (int r = 0; r < size_; ++r)
         if (!wo[r].is_same(outs[r])) outs[r].copy_(wo[r]);
+    if (co) co->run(x);
   }, icp);
   record(cname, algo, bytes, t0);
   return work;
@@ -1971,7 +858,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
 
 // =================================================================== reduce-scatter
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
-                                                                      RedOpType op, std::chrono::milliseconds to) {
+                                                                      RedOpType op, std::chrono::milliseconds to,
+                                                                      std::shared_ptr<const Coalesced> co) {
   TORCH_CHECK(op != RedOpType::PREMUL_SUM, "ProcessGroupMI355X: PREMUL_SUM is not supported");
   const auto t0 = std::chrono::steady_clock::now();
   const size_t bytes = out.nbytes();
@@ -2007,20 +895,23 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
   if (a == Algo::HOST) {
     enqueue_reduce_scatter(Algo::HOST, wi, wo, kd, ko, nd, no, nok, op, ds, current_stream(ds.device), to);
     if (!wo.is_same(out)) out.copy_(wo);
+    if (co) co->run(current_stream(ds.device));
     record(Coll::REDUCE_SCATTER, "host", bytes, t0);
-    return cpu_done(Coll::REDUCE_SCATTER, {out});
+    return cpu_done(Coll::REDUCE_SCATTER, co ? co->members : std::vector<at::Tensor>{out});
   }
   std::vector<at::Tensor> keep{out, wo};
   for (auto& i : wi) keep.push_back(i);
+  if (co) keep.insert(keep.end(), co->members.begin(), co->members.end());
   std::shared_ptr<IpcComm> icp;
   if (is_ipc(a)) {
     ipc(ds);
     icp = ds.ipc;
   }
-  auto work = gpu_issue(Coll::REDUCE_SCATTER, ds, a, keep, {out}, to,
+  auto work = gpu_issue(Coll::REDUCE_SCATTER, ds, a, keep, co ? co->members : std::vector<at::Tensor>{out}, to,
                         [=, dsp = &ds, out = out](hipStream_t x) mutable {
     enqueue_reduce_scatter(a, wi, wo, kd, ko, nd, no, nok, op, *dsp, x, to);
     if (!wo.is_same(out)) out.copy_(wo);
+    if (co) co->run(x);
   }, icp);
   record(Coll::REDUCE_SCATTER, is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
          bytes, t0);
@@ -2167,8 +1058,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
         // self-contained (copies only): the thread may outlive a group destroyed meanwhile
         const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
         std::thread([pc, store = store_, key = "pdcc/p2p/" + std::to_string(lo) + ":" + std::to_string(hi),
-                     prank = rank_ == lo ? 0 : 1, dev = ds.device, pi] {
-          pair_builder(pc, store, key, prank, dev, pi);
+                     prank = rank_ == lo ? 0 : 1, dev = ds.device, pi, init_ms = rccl_opts().init_timeout_ms] {
+          pair_builder(pc, store, key, prank, dev, pi, init_ms);
         }).detach();
       }
       if (cfg_.watchdog_ms > 0) {
@@ -2180,8 +1071,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
     }
   }
   auto work = gpu_run(cname, ds, {t, w}, {t}, to, [&](hipStream_t s) {
-    if (is_send) PDCC_NCCL(ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
-    else PDCC_NCCL(ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+    if (is_send) PDCC_NCCLC(pc->comm->get(), ncclSend(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+    else PDCC_NCCLC(pc->comm->get(), ncclRecv(w.data_ptr(), w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
     if (!is_send && !w.is_same(t)) t.copy_(w);
   }, nullptr, &pc->stream);
   record(cname, "rccl_pair", t.nbytes(), t0);
@@ -2192,12 +1083,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
 // then enqueue the ops that queued up meanwhile, in order, each after its caller's
 // stream point, and open their gates; then mark the channel ready.
 void ProcessGroupMI355X::pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store,
-                                      std::string key, int prank, int dev, int pi) {
+                                      std::string key, int prank, int dev, int pi, int64_t init_ms) {
   std::string err;
   try {
     PDCC_HIP(hipSetDevice(dev));
     const auto t0 = std::chrono::steady_clock::now();
-    auto c = std::make_shared<RcclComm>(store, key, prank, 2, dev, RcclOpts());
+    RcclOpts o;
+    o.init_timeout_ms = init_ms;  // the peer may never post its side: bounded
+    auto c = std::make_shared<RcclComm>(store, key, prank, 2, dev, o);
     std::lock_guard<std::mutex> lk(pc->mu);
     pc->comm = c;
     pc->init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2221,8 +1114,8 @@ void ProcessGroupMI355X::pair_builder(std::shared_ptr<PairChan> pc, c10::intrusi
       c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(pc->stream);
       const hipStream_t s = pc->stream.stream();
       PDCC_HIP(hipStreamWaitEvent(s, op.after, 0));
-      if (op.is_send) PDCC_NCCL(ncclSend(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
-      else PDCC_NCCL(ncclRecv(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+      if (op.is_send) PDCC_NCCLC(pc->comm->get(), ncclSend(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
+      else PDCC_NCCLC(pc->comm->get(), ncclRecv(op.w.data_ptr(), op.w.nbytes(), ncclUint8, pi, pc->comm->get(), s));
       if (!op.is_send && !op.w.is_same(op.t)) op.t.copy_(op.w);
       for (const at::Tensor* x : {&op.t, &op.w})
         c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(x->storage().data_ptr(),
@@ -2272,7 +1165,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::endCoalescing() {
     RcclComm::Issue og(*ds->rccl, s, capturing(s));
     PDCC_NCCL(ncclGroupStart());
     for (auto& f : fns) f(s);
-    PDCC_NCCL(ncclGroupEnd());
+    PDCC_NCCLC(ds->rccl->get(), ncclGroupEnd());
     for (size_t i = 0; i + 1 < keep.size(); i += 2)
       if (!keep[i].is_same(keep[i + 1])) keep[i].copy_(keep[i + 1]);
   });

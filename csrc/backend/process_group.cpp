@@ -374,6 +374,8 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
       cfg_(Config::from_env()),
       health_(std::make_shared<Health>()) {
   members_key_ = make_members_key(global_ranks_, size);
+  // an RCCL op left in progress by a non-blocking communicator is waited for at most this long
+  set_rccl_settle_timeout_ms(timeout_.count());
   if (const char* hp = std::getenv("PDCC_HOST_PROF")) hp_.on = *hp && *hp != '0';
   if (!cfg_.fault.empty()) {
     unsigned long long s = 0;
@@ -619,7 +621,7 @@ std::string ProcessGroupMI355X::describe() {
   std::lock_guard<std::mutex> lk(init_mu_);
   for (auto& kv : devs_) {
     o << ", dev" << kv.first << "{rccl_ok=" << kv.second->rccl_ok << ", ipc_ok=" << kv.second->ipc_ok
-      << ", zc_ok=" << kv.second->zc_ok << ", zx_ok=" << (kv.second->ipc ? kv.second->ipc->zx_on() : false)
+      << ", zc_ok=" << kv.second->zc_ok << ", zx_ok=" << (kv.second->ipc ? kv.second->ipc->zx_on() : kv.second->zx_ok)
       << ", zx_fast=" << (kv.second->ipc ? kv.second->ipc->zx_fast() : 0)
       << ", zx_host=" << (kv.second->ipc ? kv.second->ipc->zx_host() : 0)
       << ", ll_ok=" << kv.second->ll_ok << ", shared_device=" << kv.second->shared_device
@@ -629,6 +631,8 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
+      << ", zc_reaped=" << (kv.second->ipc ? kv.second->ipc->zc_reaped() : 0)
+      << ", async_capped=" << (kv.second->ipc ? kv.second->ipc->async_capped() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
       << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0);
     if (kv.second->launcher) {
@@ -872,22 +876,6 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce(std::vector<at::Ten
   return cpu_done(Coll::ALLREDUCE, tensors);
 }
 
-c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce_coalesced(std::vector<at::Tensor>& tensors,
-                                                                       const c10d::AllreduceCoalescedOptions& opts) {
-  c10::intrusive_ptr<c10d::Work> last;
-  for (auto& t : tensors) {
-    std::vector<at::Tensor> one{t};
-    c10d::AllreduceOptions o;
-    o.reduceOp = opts.reduceOp;
-    o.timeout = opts.timeout;
-    o.asyncOp = opts.asyncOp;
-    last = allreduce(one, o);
-  }
-  if (!last) return cpu_done(Coll::ALLREDUCE, {});
-  // all pieces ran on the same stream: waiting on the last one orders them all
-  return last;
-}
-
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce(std::vector<at::Tensor>& tensors,
                                                           const c10d::ReduceOptions& opts) {
   op_async_ = opts.asyncOp;
@@ -960,15 +948,6 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_allgather_base(at::Tensor& o
   for (int r = 0; r < size_; ++r) outs[0].push_back(flat.narrow(0, r * input.numel(), input.numel()).view(input.sizes()));
   std::vector<at::Tensor> ins{input};
   return allgather(outs, ins, opts);
-}
-
-c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather_into_tensor_coalesced(std::vector<at::Tensor>& outputs,
-                                                                                   std::vector<at::Tensor>& inputs,
-                                                                                   const c10d::AllgatherOptions& opts) {
-  TORCH_CHECK(outputs.size() == inputs.size(), "allgather_into_tensor_coalesced: list size mismatch");
-  c10::intrusive_ptr<c10d::Work> last;
-  for (size_t i = 0; i < inputs.size(); ++i) last = _allgather_base(outputs[i], inputs[i], opts);
-  return last ? last : cpu_done(Coll::ALLGATHER, {});
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gather(std::vector<std::vector<at::Tensor>>& outputs,
@@ -1072,14 +1051,6 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_reduce_scatter_base(at::Tens
   for (int r = 0; r < size_; ++r) ins[0].push_back(flat.narrow(0, r * output.numel(), output.numel()).view(output.sizes()));
   std::vector<at::Tensor> outs{output};
   return reduce_scatter(outs, ins, opts);
-}
-
-c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter_tensor_coalesced(
-    std::vector<at::Tensor>& outputs, std::vector<at::Tensor>& inputs, const c10d::ReduceScatterOptions& opts) {
-  TORCH_CHECK(outputs.size() == inputs.size(), "reduce_scatter_tensor_coalesced: list size mismatch");
-  c10::intrusive_ptr<c10d::Work> last;
-  for (size_t i = 0; i < inputs.size(); ++i) last = _reduce_scatter_base(outputs[i], inputs[i], opts);
-  return last ? last : cpu_done(Coll::REDUCE_SCATTER, {});
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::alltoall_base(at::Tensor& output, at::Tensor& input,

@@ -224,6 +224,16 @@ struct IpcLauncher {
   size_t depth_sum = 0;  // jobs still queued when a job starts (summed: mean queue depth)
 };
 
+// A coalesced collective's members (torch's _coalescing_manager fast path, all_reduce_coalesced):
+// packed into one flat buffer before the collective, unpacked from it on the collective's
+// own stream afterwards (coalesced.cpp)
+struct Coalesced {
+  std::vector<at::Tensor> members;     // kept alive, and the Work's outputs
+  std::vector<kern::CopyDesc> unpack;  // K2 descriptors flat -> contiguous members (one launch per 64)
+  std::vector<std::pair<at::Tensor, at::Tensor>> copies;  // (member, view of flat): non-contiguous members
+  void run(hipStream_t s) const;       // the unpack, on `s` (the current stream is `s` too)
+};
+
 // whether `s` is being captured into a graph (launcher.cpp)
 bool capturing_stream(hipStream_t s);
 
@@ -238,6 +248,7 @@ struct DeviceState {
   bool ipc_ok = false;                  // same host, peers reachable, 2..8 ranks
   bool zc_ok = false;                   // zero-copy IPC (user buffers read in place) passed its self-test
   bool ll_ok = false;                   // LL all-reduce (flag-tagged pushes, no barrier) passed its self-test
+  bool zx_ok = false;                   // device-side zero-copy record exchange (voted: intent AND self-test)
   bool shared_device = false;           // several ranks share one GPU (test setups)
   std::shared_ptr<RcclComm> rccl;       // lazy (fresh, split from a same-member communicator, or shared)
   std::shared_ptr<RcclComm> rccl_wide;  // lazy child of `rccl` with at least PDCC_RCCL_WIDE_CTAS channels
@@ -413,10 +424,11 @@ class ProcessGroupMI355X : public c10d::Backend {
   DeviceState& dev_state(const at::Tensor& t);
   void init_topology(DeviceState& ds);
   RcclComm& rccl(DeviceState& ds);
+  RcclComm& rccl_create(DeviceState& ds);  // (rccl(): a failure poisons the group)
   RcclComm& rccl_wide(DeviceState& ds);
   std::shared_ptr<PairChan> pair_chan(DeviceState& ds, int peer);
   static void pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store, std::string key,
-                           int prank, int dev, int pi);
+                           int prank, int dev, int pi, int64_t init_ms);
   bool pair_on_distinct_devices(DeviceState& ds, int peer);
   IpcComm& ipc(DeviceState& ds);
   RcclOpts rccl_opts() const;
@@ -483,14 +495,17 @@ class ProcessGroupMI355X : public c10d::Backend {
 
   // GPU implementations (gpu_ops.cpp)
   c10::intrusive_ptr<c10d::Work> gpu_allreduce(at::Tensor& t, c10d::ReduceOp::RedOpType op, int root, bool rooted,
-                                               std::chrono::milliseconds to);
+                                               std::chrono::milliseconds to,
+                                               std::shared_ptr<const Coalesced> co = nullptr);
   c10::intrusive_ptr<c10d::Work> gpu_broadcast(at::Tensor& t, int root, std::chrono::milliseconds to);
   c10::intrusive_ptr<c10d::Work> gpu_allgather(std::vector<at::Tensor>& outs, at::Tensor& in, int root,
-                                               bool rooted, std::chrono::milliseconds to);
+                                               bool rooted, std::chrono::milliseconds to,
+                                               std::shared_ptr<const Coalesced> co = nullptr);
   c10::intrusive_ptr<c10d::Work> gpu_scatter(at::Tensor& out, std::vector<at::Tensor>& ins, int root,
                                              std::chrono::milliseconds to);
   c10::intrusive_ptr<c10d::Work> gpu_reduce_scatter(at::Tensor& out, std::vector<at::Tensor>& ins,
-                                                    c10d::ReduceOp::RedOpType op, std::chrono::milliseconds to);
+                                                    c10d::ReduceOp::RedOpType op, std::chrono::milliseconds to,
+                                                    std::shared_ptr<const Coalesced> co = nullptr);
   c10::intrusive_ptr<c10d::Work> gpu_alltoall(std::vector<at::Tensor>& outs, std::vector<at::Tensor>& ins,
                                               bool equal_split, std::chrono::milliseconds to);
   c10::intrusive_ptr<c10d::Work> gpu_p2p(at::Tensor& t, int peer, bool is_send, std::chrono::milliseconds to);

@@ -115,7 +115,6 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
-  if (const char* zx = std::getenv("PDCC_IPC_ZX")) zx_on_ = std::atoi(zx) != 0;
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
@@ -126,6 +125,11 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     const size_t sig = granule(kern::ipc_signal_bytes());
     my_flags_ = static_cast<uint32_t*>(alloc_exportable(sig, true, mine));
     PDCC_HIP(hipMemset(my_flags_, 0, sig));
+    if (const char* ep = std::getenv("PDCC_TEST_ZX_EPOCH")) {  // test hook: start the exchange epoch near the wrap
+      const uint32_t v = (uint32_t)std::strtoul(ep, nullptr, 0);
+      PDCC_HIP(hipMemcpy(reinterpret_cast<char*>(my_flags_) + kern::kZxEpochOffset, &v, sizeof(v),
+                         hipMemcpyHostToDevice));
+    }
     PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), 64, hipHostMallocMapped | hipHostMallocCoherent));
     *err_host_ = 0;
     PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
@@ -170,6 +174,12 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
 }
 
 IpcComm::~IpcComm() {
+  {
+    std::lock_guard<std::mutex> lk(reaper_mu_);
+    reaper_stop_ = true;
+  }
+  reaper_cv_.notify_all();
+  if (reaper_.joinable()) reaper_.join();
   try {
     DeviceScope ds(device_);
     graph_mode_ = false;  // the group is gone: staging retired for captured graphs goes too
@@ -183,6 +193,7 @@ IpcComm::~IpcComm() {
     for (void* q : deferred_free_) hipFree(q);
     deferred_free_.clear();
     reap_closing(true);
+    std::lock_guard<std::mutex> il(imports_mu_);
     for (auto& peer : zc_imports_)
       for (auto& im : peer) {
         if (im.last && im.last->ev) (void)hipEventSynchronize(im.last->ev);
@@ -326,6 +337,10 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
   } else if (grid_max_ > 0 && call.grid_cap <= 0) {  // (a call may carry its own cap: IPC_WIDE)
     call.grid_cap = grid_max_;
   }
+  if (async_now_ && async_grid_ > 0) {  // overlapped with compute: leave CU slots to it
+    call.grid_cap = call.grid_cap > 0 ? std::min(call.grid_cap, async_grid_) : async_grid_;
+    ++async_capped_;
+  }
   DeviceScope ds(device_);
   PDCC_HIP(kern::ipc_launch(v, call, stream));
 }
@@ -455,8 +470,43 @@ void IpcComm::reap_closing(bool wait_all) {
   }
 }
 
+void IpcComm::reaper_kick() {
+  {
+    std::lock_guard<std::mutex> lk(reaper_mu_);
+    if (reaper_stop_) return;
+    reaper_work_ = true;
+    if (!reaper_.joinable()) reaper_ = std::thread([this] { reaper_loop(); });
+  }
+  reaper_cv_.notify_all();
+}
+
+void IpcComm::reaper_loop() {
+  (void)hipSetDevice(device_);
+  // the caller's thread may be capturing a graph meanwhile: this thread's event queries and
+  // closes must not invalidate that capture
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  std::unique_lock<std::mutex> lk(reaper_mu_);
+  while (!reaper_stop_) {
+    reaper_cv_.wait(lk, [&] { return reaper_stop_ || reaper_work_; });
+    reaper_work_ = false;
+    // poll until everything queued so far is closed (each entry waits for its last launch)
+    while (!reaper_stop_) {
+      lk.unlock();
+      const size_t before = zc_closing();
+      reap_closing(false);
+      const size_t after = zc_closing();
+      reaped_ += before > after ? before - after : 0;
+      lk.lock();
+      if (after == 0) break;
+      reaper_cv_.wait_for(lk, std::chrono::microseconds(500), [&] { return reaper_stop_; });
+    }
+  }
+}
+
 bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
   DeviceScope ds(device_);
+  std::lock_guard<std::mutex> il(imports_mu_);
   if (!tls_defer_frees_) reap_closing(false);
   // evictions first, whatever the outcome of this exchange (keeps the caches in step); an
   // in-flight kernel of this rank may still read through the mapping: the close waits for
@@ -474,6 +524,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
       zc_closing_.push_back({it->map, std::move(last), it->tab >= 0 ? r : -1, it->tab});
     }
     peer.erase(it);
+    if (tls_defer_frees_) reaper_kick();  // (this thread never closes a mapping itself)
   }
   if (!tls_defer_frees_) reap_closing(false);
   zc_cur_ids_.assign(world_, 0);
@@ -535,6 +586,7 @@ void IpcComm::launch_zc(kern::IpcCall call, const std::vector<char*>& bufs, hipS
 }
 
 void IpcComm::zc_note_launch(const std::shared_ptr<LaunchEvent>& le) {
+  std::lock_guard<std::mutex> il(imports_mu_);
   for (int r = 0; r < world_ && r < (int)zc_cur_ids_.size(); ++r) {
     if (r == rank_ || zc_cur_ids_[r] == 0) continue;
     for (auto& im : zc_imports_[r])
@@ -655,7 +707,13 @@ size_t IpcComm::zc_closing() const {
   return zc_closing_.size();
 }
 
+size_t IpcComm::zc_exports() const {
+  std::lock_guard<std::mutex> zl(zc_mu_);
+  return zc_exports_.size();
+}
+
 size_t IpcComm::zc_mappings() const {
+  std::lock_guard<std::mutex> il(imports_mu_);
   size_t n = 0;
   for (const auto& p : zc_imports_) n += p.size();
   return n;

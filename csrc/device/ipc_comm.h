@@ -22,9 +22,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../kernels/kernel_api.h"
@@ -58,6 +60,24 @@ class IpcComm {
   void set_timeout_ms(uint64_t ms) { timeout_ticks_ = ms * 100000ull; }
   // workgroup cap of every launch on distinct devices (PDCC_IPC_GRID); same on every rank
   void set_grid_max(int g) { grid_max_ = g; }
+  // workgroup cap of the launches issued inside an AsyncScope (PDCC_IPC_ASYNC_GRID: collectives
+  // on the comm stream, overlapped with compute); same on every rank (0 = none)
+  void set_async_grid(int g) { async_grid_ = g; }
+  int async_grid() const { return async_grid_; }
+  // the calling thread's launches of one async collective (RAII; the issuing thread only)
+  struct AsyncScope {
+    IpcComm* c;
+    bool saved;
+    AsyncScope(IpcComm* comm, bool on) : c(comm), saved(comm ? comm->async_now_ : false) {
+      if (c) c->async_now_ = on;
+    }
+    ~AsyncScope() {
+      if (c) c->async_now_ = saved;
+    }
+    AsyncScope(const AsyncScope&) = delete;
+    AsyncScope& operator=(const AsyncScope&) = delete;
+  };
+  uint64_t async_capped() const { return async_capped_; }
   uint64_t timeout_ms() const { return timeout_ticks_ / 100000ull; }
   // a launch was captured into a graph: sequence numbers live on the device from now on
   bool graph_mode() const { return graph_mode_; }
@@ -138,7 +158,7 @@ class IpcComm {
   void zc_note_launch(const std::shared_ptr<LaunchEvent>& ev);
   // exchange thread: open ticket `t`'s gate (ok: ptrs[r] = rank r's mapped buffer)
   void gate_publish(uint64_t t, bool ok, const std::vector<char*>& ptrs);
-  size_t zc_exports() const { return zc_exports_.size(); }
+  size_t zc_exports() const;
   size_t zc_mappings() const;
   // evicted mappings not closed yet (their last launch may still run, or no safe point came)
   size_t zc_closing() const;
@@ -154,6 +174,8 @@ class IpcComm {
   // close the evicted mappings whose last launch has finished (wait_all: wait for all);
   // synchronises the device like any hipIpcCloseMemHandle -- not on the launcher's thread
   void reap_closing(bool wait_all);
+  // mappings closed so far by the reaper thread (describe(): zc_reaped)
+  uint64_t zc_reaped() const { return reaped_.load(); }
 
  private:
   void map_staging(size_t cap);
@@ -176,7 +198,7 @@ class IpcComm {
   uint64_t gate_next_ = 0;
   std::vector<std::shared_ptr<LaunchEvent>> gate_last_;  // per slot: the launches that read it
   std::shared_ptr<EventPool> ev_pool_ = std::make_shared<EventPool>();
-  std::mutex zc_mu_;  // zc_exports_ (the caller exports, the exchange thread settles)
+  mutable std::mutex zc_mu_;  // zc_exports_ (the caller exports, the exchange thread settles)
 
  public:
   // completion of one zero-copy launch (recorded on its stream right after it)
@@ -206,7 +228,7 @@ class IpcComm {
   // records up there, see kern::ZcTable). An entry is dropped (id = 0) before its mapping is
   // queued for closing, and the close then also waits for the latest gated launch of every
   // stream at that moment (any kernel that could have read the entry was launched by then).
-  bool zx_on_ = true;  // PDCC_IPC_ZX=0: gated kernels always wait for the host gate
+  bool zx_on_ = true;  // set by the group (Config::ipc_zx, voted): off = gated kernels wait for the host gate
   uint64_t zx_tag_ = 0;  // gated launches so far (resolved slot = tag % kGateSlots)
   std::atomic<uint64_t> zx_fast_{0}, zx_host_{0}, zx_failed_{0};
   kern::ZcTable* ztab_host_ = nullptr;
@@ -228,6 +250,19 @@ class IpcComm {
   };
   mutable std::mutex closing_mu_;
   std::vector<Closing> zc_closing_;
+  // Reaper: evictions queued by the launcher's thread (which never closes a mapping itself)
+  // are closed by this thread once their last launch has finished -- so with no barrier in
+  // sight (a training loop of async bucket all-reduces over many allocations) the closing
+  // list and the mapping-table slots it holds stay bounded. Started at the first such
+  // eviction; a close may synchronise the device, which blocks only this thread.
+  void reaper_kick();
+  void reaper_loop();
+  std::thread reaper_;
+  std::mutex reaper_mu_;
+  std::condition_variable reaper_cv_;
+  bool reaper_stop_ = false, reaper_work_ = false;
+  std::atomic<uint64_t> reaped_{0};
+  mutable std::mutex imports_mu_;  // zc_imports_ (launcher thread imports, describe() counts)
   static thread_local bool tls_defer_frees_;
   std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread
   std::vector<uint64_t> zc_cur_ids_;  // per peer: the allocation id mapped by the last zc_import
@@ -244,6 +279,9 @@ class IpcComm {
   uint64_t timeout_ticks_;
   bool shared_device_;
   int grid_max_ = 0;  // 0: the kernel library's default cap
+  int async_grid_ = 0;
+  bool async_now_ = false;     // inside an AsyncScope (the group's issuing thread)
+  uint64_t async_capped_ = 0;  // launches the async cap applied to
 
   uint32_t* my_flags_ = nullptr;          // uncached device memory
   std::vector<uint32_t*> peer_flags_;     // mapped (own entry = my_flags_)

@@ -3,8 +3,10 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "comm_util.h"
@@ -27,6 +29,7 @@ struct DeviceGuard {
 
 ncclConfig_t make_config(const RcclOpts& o, bool for_split) {
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;  // creation is polled against a deadline (wait_ready)
   if (o.min_ctas > 0) cfg.minCTAs = o.min_ctas;
   if (o.max_ctas > 0) cfg.maxCTAs = o.max_ctas;
   if (for_split) cfg.splitShare = o.split_share ? 1 : 0;
@@ -39,8 +42,42 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 std::mutex g_reg_mu;
 std::map<std::string, std::weak_ptr<RcclComm>> g_reg;
+std::atomic<int64_t> g_settle_ms{600000};
+
+std::string nccl_msg(ncclResult_t r, const char* what, const char* file, int line) {
+  const char* last = ncclGetLastError(nullptr);
+  return std::string("pdcc: RCCL error '") + ncclGetErrorString(r) + "' (" + (last ? last : "") + ") in " + what +
+         " at " + file + ":" + std::to_string(line);
+}
 
 }  // namespace
+
+void set_rccl_settle_timeout_ms(int64_t ms) { g_settle_ms.store(std::max<int64_t>(1, ms)); }
+
+void nccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, const char* file, int line) {
+  if (r == ncclInProgress && comm) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t lim = g_settle_ms.load();
+    for (uint32_t it = 0;; ++it) {
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t q = ncclCommGetAsyncError(comm, &st);
+      if (q != ncclSuccess) {
+        r = q;
+        break;
+      }
+      if (st != ncclInProgress) {
+        r = st;
+        break;
+      }
+      if (ms_since(t0) > (double)lim)
+        throw std::runtime_error("pdcc: RCCL operation still in progress after " + std::to_string(lim) + " ms (" +
+                                 what + " at " + file + ":" + std::to_string(line) +
+                                 "): a peer rank is not taking part");
+      if (it > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  if (r != ncclSuccess) throw std::runtime_error(nccl_msg(r, what, file, line));
+}
 
 std::vector<std::string> forward_rccl_env() {
   static std::once_flag once;
@@ -69,23 +106,32 @@ RcclComm::RcclComm(const c10::intrusive_ptr<c10d::Store>& store, const std::stri
     : device_(device), world_(world) {
   forward_rccl_env();
   const auto t0 = std::chrono::steady_clock::now();
+  const auto deadline = t0 + std::chrono::milliseconds(opts.init_timeout_ms);
   ncclUniqueId id;
   const std::string k = key + "/rccl_uid";
   if (rank == 0) {
     PDCC_NCCL(ncclGetUniqueId(&id));
     store->set(k, std::vector<uint8_t>(reinterpret_cast<uint8_t*>(&id), reinterpret_cast<uint8_t*>(&id) + sizeof(id)));
   } else {
+    try {  // bounded: rank 0 may never get here
+      store->wait({k}, std::chrono::milliseconds(std::max<int64_t>(1, opts.init_timeout_ms)));
+    } catch (const std::exception& e) {
+      throw std::runtime_error("pdcc: RCCL communicator creation: rank 0's unique id did not arrive within " +
+                               std::to_string(opts.init_timeout_ms) + " ms (PDCC_RCCL_INIT_TIMEOUT_S): " + e.what());
+    }
     const std::vector<uint8_t> v = store->get(k);
     if (v.size() != sizeof(id)) throw std::runtime_error("pdcc: malformed RCCL unique id in store");
     std::memcpy(&id, v.data(), sizeof(id));
   }
   DeviceGuard g(device);
-  if (opts.any()) {
-    ncclConfig_t cfg = make_config(opts, false);
-    PDCC_NCCL(ncclCommInitRankConfig(&comm_, world, id, rank, &cfg));
-  } else {
-    PDCC_NCCL(ncclCommInitRank(&comm_, world, id, rank));
+  ncclConfig_t cfg = make_config(opts, false);
+  const ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    throw std::runtime_error(nccl_msg(r, "ncclCommInitRankConfig", __FILE__, __LINE__));
   }
+  wait_ready(deadline, opts.init_timeout_ms, "ncclCommInitRankConfig");
   init_ms_ = ms_since(t0);
 }
 
@@ -94,15 +140,54 @@ RcclComm::RcclComm(const RcclComm& parent, int rank, const RcclOpts& opts)
   const auto t0 = std::chrono::steady_clock::now();
   DeviceGuard g(device_);
   ncclConfig_t cfg = make_config(opts, true);
-  PDCC_NCCL(ncclCommSplit(parent.comm_, /*color=*/0, /*key=*/rank, &comm_, &cfg));
+  const ncclResult_t r = ncclCommSplit(parent.comm_, /*color=*/0, /*key=*/rank, &comm_, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
+    throw std::runtime_error(nccl_msg(r, "ncclCommSplit", __FILE__, __LINE__));
+  }
   if (!comm_) throw std::runtime_error("pdcc: ncclCommSplit returned no communicator");
+  wait_ready(t0 + std::chrono::milliseconds(opts.init_timeout_ms), opts.init_timeout_ms, "ncclCommSplit");
   init_ms_ = ms_since(t0);
+}
+
+void RcclComm::wait_ready(std::chrono::steady_clock::time_point deadline, int64_t budget_ms, const char* what) {
+  for (uint32_t it = 0;; ++it) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclSuccess) return;
+    if (st != ncclInProgress) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      throw std::runtime_error(nccl_msg(st, what, __FILE__, __LINE__));
+    }
+    if (std::chrono::steady_clock::now() > deadline) {
+      ncclCommAbort(comm_);  // unblocks RCCL's bootstrap / connection threads
+      comm_ = nullptr;
+      throw std::runtime_error(std::string("pdcc: RCCL communicator creation (") + what + ") did not complete within " +
+                               std::to_string(budget_ms) + " ms (PDCC_RCCL_INIT_TIMEOUT_S): a peer rank died or "
+                               "never joined the group");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(it < 200 ? 50 : 1000));
+  }
 }
 
 RcclComm::~RcclComm() {
   if (!comm_) return;
   if (aborted_.load()) return;  // ncclCommAbort already freed it
-  ncclCommDestroy(comm_);
+  // non-blocking communicator: finalize (flushes its work) may complete asynchronously; a
+  // peer that is gone would keep it in progress forever -- abort after a bounded wait
+  ncclResult_t r = ncclCommFinalize(comm_);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress && ms_since(t0) < 10000.0) {
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) break;
+    r = st;
+  }
+  if (r == ncclSuccess) ncclCommDestroy(comm_);
+  else ncclCommAbort(comm_);
 }
 
 void RcclComm::abort() {

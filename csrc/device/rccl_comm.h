@@ -18,6 +18,7 @@
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -36,11 +37,25 @@ namespace pdcc {
                                __FILE__ + ":" + std::to_string(__LINE__));                          \
   } while (0)
 
+// RCCL calls on a non-blocking communicator (every RcclComm is one, see below) may return
+// ncclInProgress: RCCL's own thread is still connecting channels and enqueuing the op. Wait
+// for it (bounded by the settle timeout) before returning, so the caller's stream order is
+// exactly the one a blocking communicator gives; any other result throws like PDCC_NCCL.
+// Not for calls between ncclGroupStart and ncclGroupEnd (settle the ncclGroupEnd instead).
+void nccl_settle(ncclComm_t comm, ncclResult_t r, const char* what, const char* file, int line);
+#define PDCC_NCCLC(comm, expr) ::pdcc::nccl_settle((comm), (expr), #expr, __FILE__, __LINE__)
+// upper bound of one nccl_settle wait (process-wide; the groups set it from their config)
+void set_rccl_settle_timeout_ms(int64_t ms);
+
 // Per-communicator RCCL configuration (ncclConfig_t fields); -1 = RCCL's default.
 struct RcclOpts {
   int min_ctas = -1;     // channels (one CTA each) at least / at most: 7 xGMI links per GPU
   int max_ctas = -1;
   int split_share = 1;   // ncclCommSplit children share the parent's resources
+  // Deadline of the creation (unique-id wait + init / split): communicators are created
+  // non-blocking (ncclConfig_t.blocking = 0) and polled; past the deadline the half-built
+  // communicator is aborted and the constructor throws (a peer died or never joined)
+  int64_t init_timeout_ms = 300000;
   bool any() const { return min_ctas > 0 || max_ctas > 0; }
 };
 
@@ -96,6 +111,9 @@ class RcclComm {
 
  private:
   IssueOrder order_;
+
+  // poll the non-blocking creation until it leaves ncclInProgress; abort + throw past `deadline`
+  void wait_ready(std::chrono::steady_clock::time_point deadline, int64_t budget_ms, const char* what);
 
   ncclComm_t comm_ = nullptr;
   int device_;

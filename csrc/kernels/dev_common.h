@@ -571,10 +571,13 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
   uint32_t ep = 0;
   if (lane == 0) {  // only block 0 of this rank's gated kernels touches it, in stream order
     ep = __hip_atomic_load(epw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    // never tag 0 (fresh signal memory is zero), and skip it BEFORE storing: on the wrap the
+    // stored word must move on to 1 too, or the next call would compute tag 1 again and
+    // could take the previous call's records (and vote) for its own
+    if (ep == 0u) ep = 1u;
     __hip_atomic_store(epw, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   ep = __shfl(ep, 0);
-  if (ep == 0u) ep = 1u;  // (never tag 0: fresh signal memory is zero)
   // round 1: my record into slot [me] of every rank (4 single-copy-atomic words)
   if (lane < W) {
     uint64_t* d = zx_src_words(v, lane, me);

@@ -1510,3 +1510,178 @@ def zx_steady_probe(rank, size, device="cuda", calls=100, n=(4 << 20) // 4):
     m = re.search(r"zx_fast=(\d+), zx_host=(\d+)", desc)
     return {"ok": ok, "algo": b.last_algo(), "fast": int(m.group(1)) if m else -1,
             "host": int(m.group(2)) if m else -1, "desc": desc}
+
+
+def rccl_init_deadline(rank, size, device="cuda"):
+    """Rank 1 never builds its RCCL communicator (PDCC_TEST_RCCL_INIT_SKIP): rank 0's
+    non-blocking creation must give up at PDCC_RCCL_INIT_TIMEOUT_S with a clear message,
+    poison the group, and the group's next call must fail at once (reference: Gloo surfaces a
+    dead peer in ~0.2 s; main.py:94 / main.py:11 build the communicators)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    x = torch.ones(1 << 16, device=d)
+    res = {}
+    t0 = time.time()
+    try:
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        res["first"] = "no error"
+    except RuntimeError as e:
+        res["first"] = str(e)[:400]
+    res["first_s"] = time.time() - t0
+    t1 = time.time()
+    try:
+        dist.all_reduce(x)
+        res["second"] = "no error"
+    except RuntimeError as e:
+        res["second"] = str(e)[:400]
+    res["second_s"] = time.time() - t1
+    return res
+
+
+def coalesced_probe(rank, size, device="cpu", n=64, base=4096, timing=False):
+    """Coalesced collectives (verdict r3 Next #5): torch's _coalescing_manager fast path
+    (all_reduce / all_gather_into_tensor / reduce_scatter_tensor) and dist.all_reduce_coalesced
+    run as ONE collective per call, checked against fp64 references built from every rank's
+    seeded members. Members are ragged (not multiples of 16 B), mixed-dtype for the all-gather,
+    and one all_reduce member is a non-contiguous view. Returns {check: ok} plus the number of
+    collectives the backend recorded per coalesced call (and, with timing, loop vs coalesced us)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, d.type)
+    sizes = [base + 13 * i + (i % 3) for i in range(n)] + [2 * base + 6]  # [n]: the strided member (even)
+
+    def member(i, r, dt=torch.float32):
+        g = torch.Generator().manual_seed(1000 * i + 17 * r)
+        return (torch.rand(sizes[i], generator=g, dtype=torch.float64) - 0.5).to(dt)
+
+    res = {}
+
+    def colls():
+        st = b.stats()
+        return sum(v[0] for k, v in st.items() if not k.startswith(("coalesced/", "rccl_comm/")))
+
+    # --- all_reduce through the coalescing manager (async), one strided member
+    ts = [member(i, rank).to(d) for i in range(n)]
+    strided = member(n, rank).to(d).view(2, -1).t()  # non-contiguous view of fresh storage
+    c0 = colls()
+    with dist._coalescing_manager(device=d, async_ops=True) as cm:
+        for t in ts:
+            dist.all_reduce(t)
+        dist.all_reduce(strided)
+    cm.wait()
+    res["allreduce_collectives"] = colls() - c0
+    ok = True
+    for i, t in enumerate(ts + [strided]):
+        want = sum(member(i, r).double() for r in range(size))
+        got = t.cpu().double() if i < n else t.t().reshape(-1).cpu().double()
+        ok = ok and torch.allclose(got, want, rtol=1e-5, atol=1e-6)
+    res["allreduce_ok"] = bool(ok)
+    # --- dist.all_reduce_coalesced with MAX (the older API, same backend entry point)
+    ms = [member(i, rank).to(d) for i in range(8)]
+    c0 = colls()
+    dist.all_reduce_coalesced(ms, op=dist.ReduceOp.MAX)
+    res["allreduce_coalesced_api_collectives"] = colls() - c0
+    res["allreduce_coalesced_api_ok"] = all(
+        torch.equal(m.cpu(), torch.stack([member(i, r) for r in range(size)]).max(0).values) for i, m in enumerate(ms))
+    # --- all_gather_into_tensor, mixed dtypes
+    dts = [torch.float32, torch.bfloat16, torch.int64, torch.float16]
+    ins = [member(i, rank, dts[i % 4]).to(d) for i in range(n)]
+    outs = [torch.empty(size * sizes[i], dtype=dts[i % 4], device=d) for i in range(n)]
+    c0 = colls()
+    with dist._coalescing_manager(device=d, async_ops=True) as cm:
+        for o, x in zip(outs, ins):
+            dist.all_gather_into_tensor(o, x)
+    cm.wait()
+    res["allgather_collectives"] = colls() - c0
+    res["allgather_ok"] = all(torch.equal(outs[i].cpu(), torch.cat([member(i, r, dts[i % 4]) for r in range(size)]))
+                              for i in range(n))
+    # --- reduce_scatter_tensor, SUM
+    rins = [torch.cat([member(i, 100 * rank + q) for q in range(size)]).to(d) for i in range(n)]
+    routs = [torch.empty(sizes[i], device=d) for i in range(n)]
+    c0 = colls()
+    with dist._coalescing_manager(device=d, async_ops=True) as cm:
+        for o, x in zip(routs, rins):
+            dist.reduce_scatter_tensor(o, x)
+    cm.wait()
+    res["reduce_scatter_collectives"] = colls() - c0
+    res["reduce_scatter_ok"] = all(
+        torch.allclose(routs[i].cpu().double(), sum(member(i, 100 * r + rank).double() for r in range(size)),
+                       rtol=1e-5, atol=1e-6) for i in range(n))
+    if timing:  # 64 x 16 KiB all_reduce: per-member loop vs one coalesced call
+        xs = [torch.rand(4096, device=d) for _ in range(n)]
+
+        def loop():
+            for x in xs:
+                dist.all_reduce(x)
+
+        def coal():
+            with dist._coalescing_manager(device=d, async_ops=False):
+                for x in xs:
+                    dist.all_reduce(x)
+
+        for name, fn in (("loop", loop), ("coalesced", coal)):
+            fn()
+            torch.cuda.synchronize()
+            lat = []
+            for _ in range(10):
+                dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                lat.append(time.perf_counter() - t0)
+            lat.sort()
+            res[f"{name}_us"] = lat[len(lat) // 2] * 1e6
+    dist.barrier()
+    return res
+
+
+def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(10 << 20) // 4 + 64):
+    """async zero-copy all_reduces over more allocations than the export cache holds,
+    with NO barrier anywhere: evictions queued by the exchange thread must still be closed (the
+    reaper thread), so the closing list stays bounded, and the device-side exchange keeps
+    resolving calls (zx_fast grows: mapping-table slots are recycled)."""
+    import re
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    bufs = [torch.full((n + 64 * i,), float(rank + i), device=d) for i in range(allocs)]
+    ok = True
+    closing, fast = [], []
+
+    def grab(key):
+        m = re.search(key + r"=(\d+)", b.describe())
+        return int(m.group(1)) if m else -1
+
+    for rnd in range(rounds):
+        for i, t in enumerate(bufs):
+            t.fill_(float(rank + i))
+            # twice in a row: the first call maps the fresh buffer (host gate), the second can
+            # resolve on the device -- only if a mapping-table slot was free (evictions reaped)
+            dist.all_reduce(t, async_op=True).wait()
+            dist.all_reduce(t, async_op=True).wait()
+        torch.cuda.current_stream().synchronize()
+        for i, t in enumerate(bufs):
+            ok = ok and bool(torch.all(t == sum(r + i for r in range(size)) * size))
+        time.sleep(0.05)  # (the reaper polls every 0.5 ms; give finished closes a moment)
+        closing.append(grab("zc_closing"))
+        fast.append(grab("zx_fast"))
+    return {"ok": ok, "algo": b.last_algo(), "closing": closing, "fast": fast, "reaped": grab("zc_reaped"),
+            "desc": b.describe()}

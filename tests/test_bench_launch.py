@@ -44,6 +44,15 @@ def test_bench_self_launch_prints_one_line(n):
     for name, c in conf["checks"].items():
         assert c["engine"] == "shm", (name, c)
     assert "golden/auto/reduce/PRODUCT" in conf["checks"] and "shared_comm/auto" in conf["checks"]
+    # per-section wall seconds (verdict r3 Next #1): the first multi-GPU run must explain itself
+    timing = rec["extras"]["timing"]
+    for sec in ("startup", "rendezvous", "rccl_env_sweep", "init_process_group", "first_call", "timed",
+                "p50_steps", "conformance", "total"):
+        assert sec in timing and timing[sec] >= 0, (sec, timing)
+    assert timing["total"] >= timing["timed"]
+    # the stock-RCCL comparator and the RCCL environment pre-sweep leave a skip record here
+    assert "skipped" in rec["extras"]["torch_nccl"], rec["extras"]["torch_nccl"]
+    assert "skipped" in rec["extras"]["rccl_env_sweep"], rec["extras"]["rccl_env_sweep"]
 
 
 def test_bench_failing_rank_propagates():

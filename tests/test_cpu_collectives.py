@@ -134,3 +134,14 @@ def test_conformance_pass_host_transport(world):
     for r in res:
         assert r["all_ok"], r
         assert r["passed"] >= 30 and all(c["engine"] == "shm" for c in r["checks"].values())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_coalesced_collectives_are_one_operation(world):
+    # verdict r3 Next #5: the coalescing manager's fast path and all_reduce_coalesced run as
+    # ONE collective per call (packed into one flat buffer), numerics vs an fp64 reference
+    for r in launch(W.coalesced_probe, world, args=("cpu", 16, 257)):
+        assert r["allreduce_ok"] and r["allreduce_coalesced_api_ok"], r
+        assert r["allgather_ok"] and r["reduce_scatter_ok"], r
+        assert r["allreduce_collectives"] == 1 and r["allreduce_coalesced_api_collectives"] == 1, r
+        assert r["allgather_collectives"] == 1 and r["reduce_scatter_collectives"] == 1, r
