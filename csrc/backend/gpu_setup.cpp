@@ -185,11 +185,6 @@ RcclComm& ProcessGroupMI355X::rccl(DeviceState& ds) {
 
 RcclComm& ProcessGroupMI355X::rccl_create(DeviceState& ds) {
   const auto t0 = std::chrono::steady_clock::now();
-  if (const char* h = std::getenv("PDCC_TEST_RCCL_INIT_SKIP"))  // test hook: this rank never joins
-    if (*h && std::atoi(h) == rank_) {
-      std::this_thread::sleep_for(std::chrono::milliseconds(std::max<int64_t>(0, cfg_.rccl_init_timeout_ms) + 5000));
-      throw std::runtime_error("PDCC_TEST_RCCL_INIT_SKIP: this rank skipped its communicator");
-    }
   const std::string mk = members_key_ + "@" + std::to_string(ds.device);
   std::shared_ptr<RcclComm> c;
   const char* how = "init";
@@ -212,6 +207,11 @@ RcclComm& ProcessGroupMI355X::rccl_create(DeviceState& ds) {
     }
   }
   if (!c) {
+    if (const char* h = std::getenv("PDCC_TEST_RCCL_INIT_SKIP"))  // test hook: this rank never joins RCCL
+      if (*h && std::atoi(h) == rank_) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(std::max<int64_t>(0, cfg_.rccl_init_timeout_ms) + 5000));
+        throw std::runtime_error("PDCC_TEST_RCCL_INIT_SKIP: this rank skipped its communicator");
+      }
     c = std::make_shared<RcclComm>(store_, "pdcc/rccl", rank_, size_, ds.device, rccl_opts());
     c->tag = group_name_ + "#" + mk;
   }

@@ -517,9 +517,11 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
     int32_t coll, dtype;
     int64_t numel;
     int32_t root, dev_type;
+    int32_t async_op, pad;  // async collectives may run capped grids (PDCC_IPC_ASYNC_GRID): ranks must agree
   };
   Fp mine{op_seq_.load(), (int32_t)c, ts.empty() ? -1 : (int32_t)ts[0].scalar_type(),
-          ts.empty() ? 0 : ts[0].numel(), root, ts.empty() ? -1 : (int32_t)ts[0].device().type()};
+          ts.empty() ? 0 : ts[0].numel(), root, ts.empty() ? -1 : (int32_t)ts[0].device().type(),
+          (int32_t)op_async_, 0};
   std::vector<Fp> all(size_);
   std::vector<void*> outs(size_);
   for (int r = 0; r < size_; ++r) outs[r] = &all[r];
@@ -527,12 +529,14 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
   for (int r = 0; r < size_; ++r) {
     const Fp& f = all[r];
     if (f.seq != mine.seq || f.coll != mine.coll || f.dtype != mine.dtype || f.numel != mine.numel ||
-        f.root != mine.root || f.dev_type != mine.dev_type) {
+        f.root != mine.root || f.dev_type != mine.dev_type ||
+        (f.async_op != mine.async_op && mine.dev_type == (int32_t)c10::DeviceType::CUDA)) {
       std::ostringstream o;
       o << "pdcc DEBUG: collective mismatch at op #" << mine.seq << ": rank " << rank_ << " runs "
         << coll_name(c) << "(dtype=" << mine.dtype << ", numel=" << mine.numel << ", root=" << mine.root
         << ") but rank " << r << " runs " << coll_name((Coll)f.coll) << "(dtype=" << f.dtype
-        << ", numel=" << f.numel << ", root=" << f.root << ", op #" << f.seq << ")";
+        << ", numel=" << f.numel << ", root=" << f.root << ", op #" << f.seq << ")"
+        << (f.async_op != mine.async_op ? " (async_op differs)" : "");
       throw std::runtime_error(o.str());
     }
   }
@@ -631,7 +635,7 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_exports=" << (kv.second->ipc ? kv.second->ipc->zc_exports() : 0)
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
-      << ", zc_reaped=" << (kv.second->ipc ? kv.second->ipc->zc_reaped() : 0)
+      << ", zc_full_refusals=" << (kv.second->ipc ? kv.second->ipc->zc_full_refusals() : 0)
       << ", async_capped=" << (kv.second->ipc ? kv.second->ipc->async_capped() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
       << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0);

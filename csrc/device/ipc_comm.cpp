@@ -116,6 +116,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
   zc_cache_ = std::max<size_t>(zc_cache, 1);
+  closing_limit_ = std::max<size_t>(2, (size_t)kern::kZcTab > zc_cache_ ? (size_t)kern::kZcTab - zc_cache_ : 0);
   if (world < 2 || world > kern::kMaxRanks)
     throw std::runtime_error("pdcc: the IPC path supports 2..8 ranks per group");
   DeviceScope ds(device);
@@ -174,12 +175,6 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
 }
 
 IpcComm::~IpcComm() {
-  {
-    std::lock_guard<std::mutex> lk(reaper_mu_);
-    reaper_stop_ = true;
-  }
-  reaper_cv_.notify_all();
-  if (reaper_.joinable()) reaper_.join();
   try {
     DeviceScope ds(device_);
     graph_mode_ = false;  // the group is gone: staging retired for captured graphs goes too
@@ -349,6 +344,7 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
 IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   std::lock_guard<std::mutex> zl(zc_mu_);
   ZcRec r{};
+  r.full = zc_closing() >= closing_limit_ ? 1 : 0;
   if (!p && len == 0) {  // this rank has nothing the peers read (a scatter's non-root)
     r.ok = 1;
     return r;
@@ -368,8 +364,14 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
     (void)hipGetLastError();
     return r;
   }
+  const bool full = zc_closing() >= closing_limit_;
+  r.full = full ? 1 : 0;
   auto it = std::find_if(zc_exports_.begin(), zc_exports_.end(),
                          [&](const ZcExport& e) { return e.id == id && e.base == static_cast<char*>(base); });
+  if (it == zc_exports_.end() && (full || peer_full_.load()) && !capturing) {
+    ++full_refusals_;  // no fresh export (and so no eviction) until a safe point drains the lists
+    return r;          // ok = 0: this call runs staged
+  }
   if (it == zc_exports_.end()) {
     ZcExport e{};
     e.id = id;
@@ -470,40 +472,6 @@ void IpcComm::reap_closing(bool wait_all) {
   }
 }
 
-void IpcComm::reaper_kick() {
-  {
-    std::lock_guard<std::mutex> lk(reaper_mu_);
-    if (reaper_stop_) return;
-    reaper_work_ = true;
-    if (!reaper_.joinable()) reaper_ = std::thread([this] { reaper_loop(); });
-  }
-  reaper_cv_.notify_all();
-}
-
-void IpcComm::reaper_loop() {
-  (void)hipSetDevice(device_);
-  // the caller's thread may be capturing a graph meanwhile: this thread's event queries and
-  // closes must not invalidate that capture
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
-  std::unique_lock<std::mutex> lk(reaper_mu_);
-  while (!reaper_stop_) {
-    reaper_cv_.wait(lk, [&] { return reaper_stop_ || reaper_work_; });
-    reaper_work_ = false;
-    // poll until everything queued so far is closed (each entry waits for its last launch)
-    while (!reaper_stop_) {
-      lk.unlock();
-      const size_t before = zc_closing();
-      reap_closing(false);
-      const size_t after = zc_closing();
-      reaped_ += before > after ? before - after : 0;
-      lk.lock();
-      if (after == 0) break;
-      reaper_cv_.wait_for(lk, std::chrono::microseconds(500), [&] { return reaper_stop_; });
-    }
-  }
-}
-
 bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool all_ok, std::vector<char*>& ptrs) {
   DeviceScope ds(device_);
   std::lock_guard<std::mutex> il(imports_mu_);
@@ -524,11 +492,20 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
       zc_closing_.push_back({it->map, std::move(last), it->tab >= 0 ? r : -1, it->tab});
     }
     peer.erase(it);
-    if (tls_defer_frees_) reaper_kick();  // (this thread never closes a mapping itself)
   }
   if (!tls_defer_frees_) reap_closing(false);
   zc_cur_ids_.assign(world_, 0);
+  bool any_full = false, fresh = false;
+  for (int r = 0; r < world_; ++r) {
+    any_full = any_full || all[r].full;
+    fresh = fresh || (all[r].fresh && all[r].id != 0);
+  }
+  peer_full_.store(any_full);
   if (!all_ok) return false;
+  if (any_full && fresh) {  // a rank cannot take another mapping before a safe point: staged
+    ++full_refusals_;
+    return false;
+  }
   ptrs.assign(world_, nullptr);
   if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: import (%zu closing)\n", rank_, zc_closing_.size());
   bool ok = true;

@@ -22,11 +22,9 @@
 
 #include <algorithm>
 #include <atomic>
-#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../kernels/kernel_api.h"
@@ -111,7 +109,8 @@ class IpcComm {
   struct ZcRec {
     uint8_t ok;     // 1 = exportable: 16-B aligned, inside one allocation, handle obtained
     uint8_t fresh;  // 1 = the peers have not confirmed a mapping of `id` yet
-    uint8_t pad[6];
+    uint8_t full;   // 1 = this rank's list of evicted-but-open mappings is at its limit (no fresh imports)
+    uint8_t pad[5];
     uint64_t id;
     uint64_t evict;  // allocation id the exporter dropped (0 = none): importers unmap it
     uint64_t off;    // byte offset of the buffer in its allocation
@@ -174,8 +173,9 @@ class IpcComm {
   // close the evicted mappings whose last launch has finished (wait_all: wait for all);
   // synchronises the device like any hipIpcCloseMemHandle -- not on the launcher's thread
   void reap_closing(bool wait_all);
-  // mappings closed so far by the reaper thread (describe(): zc_reaped)
-  uint64_t zc_reaped() const { return reaped_.load(); }
+  // fresh exports refused / not made because some rank's closing list was full (describe())
+  uint64_t zc_full_refusals() const { return full_refusals_.load(); }
+  size_t zc_closing_limit() const { return closing_limit_; }
 
  private:
   void map_staging(size_t cap);
@@ -250,18 +250,19 @@ class IpcComm {
   };
   mutable std::mutex closing_mu_;
   std::vector<Closing> zc_closing_;
-  // Reaper: evictions queued by the launcher's thread (which never closes a mapping itself)
-  // are closed by this thread once their last launch has finished -- so with no barrier in
-  // sight (a training loop of async bucket all-reduces over many allocations) the closing
-  // list and the mapping-table slots it holds stay bounded. Started at the first such
-  // eviction; a close may synchronise the device, which blocks only this thread.
-  void reaper_kick();
-  void reaper_loop();
-  std::thread reaper_;
-  std::mutex reaper_mu_;
-  std::condition_variable reaper_cv_;
-  bool reaper_stop_ = false, reaper_work_ = false;
-  std::atomic<uint64_t> reaped_{0};
+  // Bound on that list. Evictions made while gated launches may be in flight are only queued:
+  // closing a mapping synchronises the device, and the gated kernels wait for the exchange
+  // thread (a close from any thread while they run can deadlock in the runtime -- measured:
+  // a background closer thread hung the eviction churn test). Safe points (barrier /
+  // maintain(), inline exchanges) drain the list. Between them it is bounded instead: a rank
+  // whose list is full says so in its record (ZcRec::full); from then on no rank makes a
+  // fresh export (nothing new to map, nothing evicted) and fresh imports are refused -- such
+  // calls run staged -- while buffers every rank has mapped keep running zero-copy and
+  // resolving on the device. limit = kZcTab - cache: live + closing mappings always fit the
+  // device-side mapping table.
+  size_t closing_limit_ = 16;
+  std::atomic<bool> peer_full_{false};      // some rank reported `full` in the last exchange
+  std::atomic<uint64_t> full_refusals_{0};
   mutable std::mutex imports_mu_;  // zc_imports_ (launcher thread imports, describe() counts)
   static thread_local bool tls_defer_frees_;
   std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread

@@ -140,14 +140,36 @@ RcclComm::RcclComm(const RcclComm& parent, int rank, const RcclOpts& opts)
   const auto t0 = std::chrono::steady_clock::now();
   DeviceGuard g(device_);
   ncclConfig_t cfg = make_config(opts, true);
-  const ncclResult_t r = ncclCommSplit(parent.comm_, /*color=*/0, /*key=*/rank, &comm_, &cfg);
+  const auto deadline = t0 + std::chrono::milliseconds(opts.init_timeout_ms);
+  // A non-blocking split hands the child back through `*slot` only when RCCL's own thread has
+  // finished building it. The slot is heap memory that is deliberately leaked if we give up:
+  // that thread may still write it after this constructor has thrown.
+  auto* slot = new ncclComm_t(nullptr);
+  const ncclResult_t r = ncclCommSplit(parent.comm_, /*color=*/0, /*key=*/rank, slot, &cfg);
   if (r != ncclSuccess && r != ncclInProgress) {
-    if (comm_) ncclCommAbort(comm_);
-    comm_ = nullptr;
+    if (*slot) ncclCommAbort(*slot);
+    delete slot;
     throw std::runtime_error(nccl_msg(r, "ncclCommSplit", __FILE__, __LINE__));
   }
-  if (!comm_) throw std::runtime_error("pdcc: ncclCommSplit returned no communicator");
-  wait_ready(t0 + std::chrono::milliseconds(opts.init_timeout_ms), opts.init_timeout_ms, "ncclCommSplit");
+  for (uint32_t it = 0;; ++it) {
+    ncclComm_t c = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    if (c) {
+      comm_ = c;
+      delete slot;
+      break;
+    }
+    // (RCCL returns ncclSuccess at once for a non-blocking split and sets the slot when its
+    // job is done: "newcomm is NCCL_COMM_NULL until the split fully completes")
+    ncclResult_t st = ncclSuccess;  // a failed split job reports on the parent
+    if (ncclCommGetAsyncError(parent.comm_, &st) == ncclSuccess && st != ncclSuccess && st != ncclInProgress)
+      throw std::runtime_error(nccl_msg(st, "ncclCommSplit (async)", __FILE__, __LINE__));
+    if (std::chrono::steady_clock::now() > deadline)
+      throw std::runtime_error("pdcc: RCCL communicator creation (ncclCommSplit) did not complete within " +
+                               std::to_string(opts.init_timeout_ms) + " ms (PDCC_RCCL_INIT_TIMEOUT_S): a peer rank "
+                               "died or never joined the group");
+    std::this_thread::sleep_for(std::chrono::microseconds(it < 200 ? 50 : 1000));
+  }
+  wait_ready(deadline, opts.init_timeout_ms, "ncclCommSplit");
   init_ms_ = ms_since(t0);
 }
 

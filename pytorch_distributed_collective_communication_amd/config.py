@@ -19,6 +19,8 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_ZC_ASYNC | 1 | zero-copy calls exchange their buffer records on a per-device launcher thread: the caller's host never waits for its peers (0: inline exchange) |
 | PDCC_IPC_LL_MAX | 256K | collectives up to this size per rank / chunk (max 256K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
+| PDCC_IPC_ASYNC_GRID | 0 | workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; must agree across ranks like async_op itself (0: no cap) |
+| PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
@@ -26,6 +28,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_AUTOTUNE_COLLS | all | comma list of collectives to tune (allreduce, reduce, broadcast, allgather, gather, scatter, reduce_scatter, alltoall) |
 | PDCC_AUTOTUNE_SPIN_MS | 10000 | spin bound of IPC runs during tuning; a timeout drops IPC for that key and keeps the group healthy |
 | PDCC_AUTOTUNE_FILE | "" | persisted decisions: keys with a line in this file (same topology signature on every rank) take the recorded engine without a race; rank 0 appends every new race's verdict |
+| PDCC_RCCL_INIT_TIMEOUT_S | 300 | deadline of one RCCL communicator creation (non-blocking init / split, polled; capped by the group timeout): a peer that never joins fails the group with a clear error, later calls fail at once |
 | PDCC_RCCL_MIN_CTAS / _MAX_CTAS | -1 / -1 | RCCL channel (CTA) bounds via ``ncclCommInitRankConfig``; -1 leaves RCCL's topology tuner in charge |
 | PDCC_RCCL_GROUP_COMM | share | groups with the same members as a live communicator: share it, split from it (ncclCommSplit) or init a fresh one |
 | PDCC_RCCL_SPLIT_SHARE | 1 | ncclCommSplit children share the parent's resources |
@@ -47,6 +50,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_FLIGHT_RECORDER | 256 | number of recent collectives kept for post-mortem dumps |
 | PDCC_FAULT | "" | fault injection ``rank:op_seq:kind`` (kind exit, raise, hang) |
 | PDCC_TEST_AUTOTUNE_DELAY | "" | test hook ``rank:ms``: that rank starts its IPC tuning run late |
+| PDCC_TEST_RCCL_INIT_SKIP / _RCCL_SHARED / _ZX_EPOCH | "" | test hooks: that rank never builds its communicator / claim RCCL on a shared GPU / start the device exchange epoch at this value |
 | PDCC_TAKEOVER_GLOO / _NCCL | 0 | serve ``init_process_group("gloo"/"nccl")`` with mi355x |
 """
 from __future__ import annotations
@@ -85,6 +89,8 @@ class Config:
     ipc_ll_max: int = 256 << 10
     ipc_zc_cache: int = 16
     ipc_zc_async: bool = True
+    ipc_zx: bool = True
+    ipc_async_grid: int = 0
     ipc_spin_ms: int = 600000
     ipc_grid: int = 512
     ipc_wide_grid: int = 1024
@@ -95,6 +101,7 @@ class Config:
     autotune_colls: str = "all"
     autotune_spin_ms: int = 10000
     autotune_file: str = ""
+    rccl_init_timeout_s: int = 300
     rccl_min_ctas: int = -1
     rccl_max_ctas: int = -1
     rccl_wide_ctas: int = 112
@@ -124,7 +131,8 @@ _ENV = {
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
-    "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC", "autotune": "PDCC_AUTOTUNE",
+    "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC",
+    "ipc_zx": "PDCC_IPC_ZX", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",

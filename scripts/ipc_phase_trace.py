@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Where the time of one big IPC all_reduce goes (verdict r3 Next #7): device phase trace
+of the 2-shot all_reduce (zero-copy and staged) with W ranks sharing ONE GPU, next to K1
+(the same 2-source reduce the pull phase does) at the same workgroup budget.
+
+PDCC_IPC_TRACE records block 0's s_memrealtime stamps (100 MHz) per launch
+(kern::kTraceWords): [1] entry, [2] arrival barrier, [3] gate passed / staged,
+[4] data barrier, [5] phase 1 (reduce own tiles) done, [6] second barrier, [7] exit.
+Per phase the median over the timed calls, in microseconds, plus the HBM traffic
+model of each protocol and the rates it implies:
+
+* zero-copy 2-shot, per rank: phase 1 reads W own-tile slices (one per rank's tensor)
+  and writes S/W in place; phase 2 copies the (W-1)/W peer-owned part:
+  reads S(1 + (W-1)/W) ... writes S; W ranks share the GPU's HBM.
+* staged: + the staging copy (read S, write S) and phase 2 from staging.
+
+Ranks sharing one GPU run each IPC grid at 256 / W workgroups (co-residency: every
+block spins on its peer block), so K1 is timed at the same total workgroup count.
+
+    python scripts/ipc_phase_trace.py [--world 2] [--mib 256] [--iters 10]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def work(rank, size, mib, iters):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd import ops
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    b = be.native_backend(None, "cuda")
+    n = (mib << 20) // 4
+    x = torch.full((n,), float(rank + 1), device=dev)
+    for _ in range(3):
+        dist.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    walls = []
+    for _ in range(iters):
+        x.fill_(float(rank + 1))
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+    ok = bool(torch.all(x == size * (size + 1) / 2).item())
+    recs = [r for r in b.ipc_trace() if r[1] and r[7]][-iters:]
+
+    def ph(a, c):
+        v = [(r[c] - r[a]) / 100.0 for r in recs if r[a] and r[c] and r[c] >= r[a]]
+        return round(statistics.median(v), 1) if v else None
+
+    phases = {"entry_to_arrival": ph(1, 2), "arrival_to_data_barrier": ph(2, 4), "stage_or_gate": ph(2, 3),
+              "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7)}
+    out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
+           "phases_us": phases, "records": len(recs)}
+    # K1 at the same total workgroup budget: rank 0 alone, the others wait
+    dist.barrier()
+    if rank == 0:
+        s = [torch.rand(n // size, device=dev) for _ in range(2)]
+        o = torch.empty(n // size, device=dev)
+        k1 = {}
+        for blocks in (256 // size, 256, 0):
+            for _ in range(2):
+                ops.reduce_nway(s, out=o, impl="lds_ntl", max_blocks=blocks)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(10):
+                ops.reduce_nway(s, out=o, impl="lds_ntl", max_blocks=blocks)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 10
+            k1[f"k1_2src_{blocks or 'default'}wg_GBps"] = round(3 * o.numel() * 4 / dt / 1e9, 1)
+        out["k1"] = k1
+    dist.barrier()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--mib", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--modes", default="zc,staged")
+    a = ap.parse_args()
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+
+    S = a.mib << 20
+    W = a.world
+    for mode in a.modes.split(","):
+        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_TRACE": "64", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
+               "PDCC_AUTOTUNE": "0"}
+        res = launch(work, W, args=(a.mib, a.iters), bind_device=True, timeout_s=120, env=env, join_timeout_s=400)
+        # HBM bytes per call, all ranks together (one GPU): reads / writes
+        if mode == "zc":
+            rd, wr = W * S * (1 + (W - 1) / W), W * S
+        else:
+            rd, wr = W * S * (2 + (W - 1) / W), W * S * (1 + 1 + 1 / W)
+        for r in res:
+            r.update(mode=mode, world_on_one_gpu=W, bytes=S, hbm_read_bytes=int(rd), hbm_write_bytes=int(wr))
+            kt = r["phases_us"]["kernel_total"]
+            if kt:
+                r["hbm_TBps_kernel"] = round((rd + wr) / (kt * 1e-6) / 1e12, 2)
+            p1 = r["phases_us"]["phase1_reduce"]
+            if p1:  # phase 1 alone: every rank reads W slices of S/W and writes S/W
+                r["hbm_TBps_phase1"] = round(W * (S + S / W) / (p1 * 1e-6) / 1e12, 2)
+            print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -16,6 +16,11 @@ bracketed by cuda.synchronize), the optimizer/collective tail after backward,
 and the optimizer-state bytes each rank holds. One JSON line per mode.
 
     python scripts/zero_bench.py [--world 2] [--layers 24] [--dim 4096] [--steps 8]
+        [--async-grids 0,64,32] [--repeat 2]
+
+``--async-grids``: one run per PDCC_IPC_ASYNC_GRID value (workgroup cap of the IPC launches
+of async collectives -- the overlapped buckets; 0 = uncapped). Each line also reports
+which engines served the collectives (per-engine call counts of the default group).
 """
 import argparse
 import json
@@ -84,6 +89,11 @@ def work(rank, size, mode, layers, dim, steps, batch):
         if i >= 2:
             times.append(t2 - t0)
             tails.append(t2 - t1)
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    nb = be.native_backend(None, "cuda")
+    engines = {k: v[0] for k, v in nb.stats().items() if v[0] and not k.startswith(("rccl_comm", "coalesced"))}
+    capped = nb.describe().split("async_capped=")[1].split(",")[0] if "async_capped=" in nb.describe() else "?"
     t = torch.tensor([statistics.median(times), statistics.median(tails)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     # replicas must agree after the steps
@@ -94,7 +104,8 @@ def work(rank, size, mode, layers, dim, steps, batch):
     return {"mode": mode, "world": size, "params": sum(p.numel() for p in model.parameters()),
             "step_ms": round(t[0].item() * 1e3, 2), "after_backward_ms": round(t[1].item() * 1e3, 2),
             "opt_state_bytes_per_rank": opt.sharded_state_bytes(), "replicas_agree": same,
-            "overlapped_buckets": getattr(opt, "overlapped", None)}
+            "overlapped_buckets": getattr(opt, "overlapped", None), "engines": engines,
+            "async_grid": int(os.environ.get("PDCC_IPC_ASYNC_GRID", "0")), "async_capped_launches": capped}
 
 
 def main():
@@ -105,13 +116,21 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--modes", default="zero,zero_nooverlap,ddp")
+    ap.add_argument("--async-grids", default="0")
+    ap.add_argument("--repeat", type=int, default=1)
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
-    for mode in a.modes.split(","):
-        res = launch(work, a.world, args=(mode, a.layers, a.dim, a.steps, a.batch), bind_device=True,
-                     timeout_s=300, join_timeout_s=600)
-        print(json.dumps(res[0]), flush=True)
+    for rep in range(a.repeat):
+        for grid in a.async_grids.split(","):
+            os.environ["PDCC_IPC_ASYNC_GRID"] = grid
+            for mode in a.modes.split(","):
+                if grid != a.async_grids.split(",")[0] and mode == "zero_nooverlap":
+                    continue  # nothing runs async without the overlap: one baseline per repeat
+                res = launch(work, a.world, args=(mode, a.layers, a.dim, a.steps, a.batch), bind_device=True,
+                             timeout_s=300, join_timeout_s=600)
+                res[0]["repeat"] = rep
+                print(json.dumps(res[0]), flush=True)
 
 
 if __name__ == "__main__":

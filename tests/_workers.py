@@ -1649,11 +1649,11 @@ def coalesced_probe(rank, size, device="cpu", n=64, base=4096, timing=False):
 
 def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(10 << 20) // 4 + 64):
     """async zero-copy all_reduces over more allocations than the export cache holds,
-    with NO barrier anywhere: evictions queued by the exchange thread must still be closed (the
-    reaper thread), so the closing list stays bounded, and the device-side exchange keeps
-    resolving calls (zx_fast grows: mapping-table slots are recycled)."""
+    with NO barrier anywhere (evicted mappings can only be closed at safe points): the list of
+    evicted-but-open mappings must stay bounded (a full rank refuses fresh exports / imports, those
+    calls run staged), every result exact, and a hot buffer reduced between them keeps running
+    zero-copy and resolving on the device (zx_fast grows round after round)."""
     import re
-    import time
 
     import torch
     import torch.distributed as dist
@@ -1663,8 +1663,9 @@ def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(
     d = _dev(device)
     b = be.native_backend(None, "cuda")
     bufs = [torch.full((n + 64 * i,), float(rank + i), device=d) for i in range(allocs)]
+    hot = torch.empty(n, device=d)
     ok = True
-    closing, fast = [], []
+    closing, fast, hot_algo = [], [], []
 
     def grab(key):
         m = re.search(key + r"=(\d+)", b.describe())
@@ -1673,15 +1674,15 @@ def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(
     for rnd in range(rounds):
         for i, t in enumerate(bufs):
             t.fill_(float(rank + i))
-            # twice in a row: the first call maps the fresh buffer (host gate), the second can
-            # resolve on the device -- only if a mapping-table slot was free (evictions reaped)
             dist.all_reduce(t, async_op=True).wait()
-            dist.all_reduce(t, async_op=True).wait()
+            hot.fill_(float(rank + 1))
+            dist.all_reduce(hot, async_op=True).wait()
+            hot_algo.append(b.last_algo())
         torch.cuda.current_stream().synchronize()
         for i, t in enumerate(bufs):
-            ok = ok and bool(torch.all(t == sum(r + i for r in range(size)) * size))
-        time.sleep(0.05)  # (the reaper polls every 0.5 ms; give finished closes a moment)
+            ok = ok and bool(torch.all(t == sum(r + i for r in range(size))))
+        ok = ok and bool(torch.all(hot == size * (size + 1) / 2))
         closing.append(grab("zc_closing"))
         fast.append(grab("zx_fast"))
-    return {"ok": ok, "algo": b.last_algo(), "closing": closing, "fast": fast, "reaped": grab("zc_reaped"),
-            "desc": b.describe()}
+    return {"ok": ok, "closing": closing, "fast": fast, "refusals": grab("zc_full_refusals"),
+            "hot_algo": sorted(set(hot_algo[allocs:])), "desc": b.describe()}

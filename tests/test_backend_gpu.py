@@ -537,15 +537,15 @@ def test_coalesced_collectives_one_launch(world):
 
 
 def test_zero_copy_churn_without_barrier_stays_bounded():
-    # no barrier / maintain() anywhere -- evicted mappings are closed by the
-    # reaper thread once their last launch is done; closing stays bounded round after round
+    # no barrier / maintain() anywhere -- evicted mappings cannot be closed
+    # (a close synchronises the device while gated kernels wait for the exchange thread), so the
+    # list is bounded instead: kZcTab (32) - cache (4) = 28 entries, fresh exports refused beyond
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": "4"}
     for r in _gpu_launch(W.zc_churn_nobarrier_probe, 2, env=env, timeout_s=120):
-        assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
-        assert max(r["closing"]) <= 8, r
-        assert r["reaped"] > 0, r
-        # 96 distinct mappings went through 32 table slots per peer: later rounds still resolve
-        # their second calls on the device only because closed mappings free their slots
+        assert r["ok"], r
+        assert max(r["closing"]) <= 28 + 2, r
+        assert r["refusals"] > 0, r
+        assert r["hot_algo"] == ["ipc_2shot_zc"], r
         assert r["fast"][-1] > r["fast"][1] > 0, r
 
 
