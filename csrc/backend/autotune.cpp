@@ -118,6 +118,9 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   bool has_ipc = false;
   for (Algo a : cands) has_ipc = has_ipc || is_ipc(a);
   Spin spin(has_ipc ? ds.ipc.get() : nullptr, (uint64_t)cfg_.autotune_spin_ms, tuning_);
+  // an async call's key is raced with the grid its IPC launches will run at (PDCC_IPC_ASYNC_GRID):
+  // the verdict must hold for the capped engine next to compute, not for the full grid
+  IpcComm::AsyncScope async_cap(has_ipc ? ds.ipc.get() : nullptr, op_async_ && cfg_.ipc_async_grid > 0);
   // 0) warm-up: one run each (staging growth, first-touch), then check every result
   //    against the reference engine's on identical data
   for (size_t k = 0; k < n; ++k) {

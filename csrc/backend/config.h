@@ -56,8 +56,11 @@ struct Config {
   // Workgroup cap of IPC / LL launches issued on the comm stream (async_op=True collectives,
   // e.g. DDP / ZeRO buckets overlapped with backward): the kernels spin in cross-GPU
   // barriers while a peer lags, holding CU slots that the overlapped GEMMs need. 0 = no cap
-  // (the synchronous cap PDCC_IPC_GRID applies).
-  int ipc_async_grid = 0;                  // PDCC_IPC_ASYNC_GRID
+  // (the synchronous cap PDCC_IPC_GRID applies). 64: scripts/zero_bench.py, 403 M-param bf16 step, two
+  // ranks on one MI355X (profiles/r4/zero_bench_async_grid_r4.jsonl): replicated DP 36.4-36.7 ms at 64
+  // vs 37.2-37.5 uncapped, ZeRO 30.8-31.2 either way, 32 worse; 64 workgroups still keep ~4 MiB of
+  // remote loads in flight per GPU at W = 8 -- about RCCL's own CTA footprint for a collective.
+  int ipc_async_grid = 64;                 // PDCC_IPC_ASYNC_GRID
   // Zero-copy calls exchange their records on a per-device launcher thread (IpcLauncher in
   // process_group.h): the caller's host never waits for its peers (0 = inline exchange)
   bool ipc_zc_async = true;                // PDCC_IPC_ZC_ASYNC

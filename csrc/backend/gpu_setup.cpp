@@ -2,6 +2,8 @@
 // the RCCL communicators (fresh / split / shared / wide / point-to-point pairs), the
 // IPC communicator and its self-test (the reference's
 // init_process_group + new_group, main.py:11,21,31,46,63,75,94).
+#include <cstring>
+
 #include "gpu_util.h"
 
 namespace pdcc {
@@ -120,6 +122,28 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
   const auto votes = store_allgather(store_, "pdcc/dev_ipc", rank_, size_, std::vector<uint8_t>{(uint8_t)ok});
   for (const auto& v : votes) ok = ok && !v.empty() && v[0] == 1;
 
+  // The IPC workgroup caps must be the same on every rank (the block-pairwise protocol pairs block b of
+  // every rank): a rank started with different PDCC_IPC_GRID / _WIDE_GRID / _ASYNC_GRID settings is
+  // brought to the group's minimum instead of hanging its peers' barriers.
+  {
+    const int32_t mine3[3] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid};
+    const auto gv = store_allgather(store_, "pdcc/dev_grids", rank_, size_,
+                                    std::vector<uint8_t>(reinterpret_cast<const uint8_t*>(mine3),
+                                                         reinterpret_cast<const uint8_t*>(mine3) + sizeof(mine3)));
+    int32_t lo[3] = {mine3[0], mine3[1], mine3[2]};
+    for (const auto& v : gv) {
+      if (v.size() != sizeof(mine3)) continue;
+      int32_t t[3];
+      std::memcpy(t, v.data(), sizeof(t));
+      for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], t[k]);
+    }
+    if (lo[0] != mine3[0] || lo[1] != mine3[1] || lo[2] != mine3[2])
+      fprintf(stderr, "[pdcc r%d] IPC grid caps differ between ranks: using the group minimum %d/%d/%d\n", rank_,
+              lo[0], lo[1], lo[2]);
+    cfg_.ipc_grid = std::max(1, lo[0]);
+    cfg_.ipc_wide_grid = lo[1];
+    cfg_.ipc_async_grid = lo[2];
+  }
   ds.recs = recs;
   ds.shared_device = shared;
   ds.rccl_ok = !shared;

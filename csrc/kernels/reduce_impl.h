@@ -21,10 +21,13 @@ struct Ptrs8 {
   int ntl;      // K1 source loads non-temporal
 };
 
-// LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU)
+// LDS ring depth per source count: keeps DEPTH*NSRC*4KiB <= 64 KiB (2 blocks/CU). Two sources
+// (W = 2) take 6 tiles (48 KiB): the bytes in flight per workgroup set the rate (Little's law),
+// and at depth 4 the zero-copy all-reduce's reduce phase ran at 4.2-4.4 TB/s on one GPU where K1
+// at the same workgroup budget and depth 6 reaches 6.3 (profiles/r4/ipc_phase_trace_w2.jsonl).
 template <int NSRC>
 struct DepthFor {
-  static constexpr int value = NSRC <= 2 ? 4 : (NSRC <= 4 ? 3 : 2);
+  static constexpr int value = NSRC <= 2 ? 6 : (NSRC <= 4 ? 3 : 2);
 };
 
 // --------------------------------------------------------------------------- K1

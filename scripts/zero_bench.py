@@ -105,7 +105,7 @@ def work(rank, size, mode, layers, dim, steps, batch):
             "step_ms": round(t[0].item() * 1e3, 2), "after_backward_ms": round(t[1].item() * 1e3, 2),
             "opt_state_bytes_per_rank": opt.sharded_state_bytes(), "replicas_agree": same,
             "overlapped_buckets": getattr(opt, "overlapped", None), "engines": engines,
-            "async_grid": int(os.environ.get("PDCC_IPC_ASYNC_GRID", "0")), "async_capped_launches": capped}
+            "async_grid": int(os.environ.get("PDCC_IPC_ASYNC_GRID", "64")), "async_capped_launches": capped}
 
 
 def main():
@@ -116,7 +116,7 @@ def main():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--modes", default="zero,zero_nooverlap,ddp")
-    ap.add_argument("--async-grids", default="0")
+    ap.add_argument("--async-grids", default="64", help="comma list of PDCC_IPC_ASYNC_GRID values (0: uncapped)")
     ap.add_argument("--repeat", type=int, default=1)
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch

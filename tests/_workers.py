@@ -1686,3 +1686,40 @@ def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(
         fast.append(grab("zx_fast"))
     return {"ok": ok, "closing": closing, "fast": fast, "refusals": grab("zc_full_refusals"),
             "hot_algo": sorted(set(hot_algo[allocs:])), "desc": b.describe()}
+
+def async_grid_probe(rank, size, device="cuda", calls=6):
+    """PDCC_IPC_ASYNC_GRID: async_op=True IPC launches run the capped grid (counted in
+    describe(): async_capped), synchronous ones do not; every result exact."""
+    import re
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok = True
+
+    def capped():
+        m = re.search(r"async_capped=(\d+)", b.describe())
+        return int(m.group(1)) if m else -1
+
+    res = {}
+    for n in (1000, (4 << 20) // 4 + 7):  # LL and zero-copy 2-shot (+ staged rest)
+        x = torch.empty(n, device=d)
+        c0 = capped()
+        for _ in range(calls):
+            x.fill_(float(rank + 1))
+            dist.all_reduce(x)
+            ok = ok and bool(torch.all(x == size * (size + 1) / 2))
+        res[f"sync_capped_{n}"] = capped() - c0
+        c0 = capped()
+        for _ in range(calls):
+            x.fill_(float(rank + 1))
+            dist.all_reduce(x, async_op=True).wait()
+            ok = ok and bool(torch.all(x == size * (size + 1) / 2))
+        res[f"async_capped_{n}"] = capped() - c0
+    torch.cuda.synchronize()
+    res["ok"] = ok
+    return res

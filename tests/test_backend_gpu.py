@@ -557,3 +557,16 @@ def test_zero_copy_device_exchange_epoch_wraps():
     for r in _gpu_launch(W.zx_steady_probe, 2, args=("cuda", 100), env=env, timeout_s=120):
         assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
         assert r["fast"] >= 30, (r["fast"], r["host"], r["desc"])
+
+
+def test_async_collectives_take_the_capped_grid():
+    # verdict r3 Next #4: PDCC_IPC_ASYNC_GRID caps the IPC / LL launches of async_op=True
+    # collectives (overlapped with compute); synchronous ones keep the full grid
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ASYNC_GRID": "16"}
+    for r in _gpu_launch(W.async_grid_probe, 2, env=env, timeout_s=120):
+        assert r["ok"], r
+        for k, v in r.items():
+            if k.startswith("sync_capped"):
+                assert v == 0, r
+            elif k.startswith("async_capped"):
+                assert v >= 6, r
