@@ -291,6 +291,8 @@ def run_rank(args):
             },
             "correct": correct,
             "data_finite": finite,
+            # torch's own ProcessGroupNCCL on the same 1 GiB all_reduce (extras.torch_nccl): its p50 / ours
+            "vs_torch_nccl": _vs_torch_nccl_headline(extras, p50),
             "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
             "extras": extras,
         }
@@ -808,6 +810,14 @@ def torch_nccl_compare(world, rank, dev, native, x):
     finally:
         dist.destroy_process_group(g)
     return {"rows": rows}
+
+
+def _vs_torch_nccl_headline(extras, p50_s):
+    try:
+        row = extras["torch_nccl"]["rows"]["all_reduce_1GiB"]
+        return round(row["p50_ms"] / (p50_s * 1e3), 3) if p50_s > 0 and not SMALL else None
+    except (KeyError, TypeError):
+        return None
 
 
 def vs_torch_nccl(ours: dict, theirs: dict) -> dict:

@@ -332,6 +332,18 @@ __device__ __forceinline__ void ipc_pipe(char* lds, const Map& m, int avg_div) {
   pipe_run<DT, OP, NSRC, DEPTH, Map, NDST, false, PDCC_IPC_NTL != 0>(lds, m, avg_div);
 }
 
+// Zero-copy reductions read every rank's tensor exactly once per call (the reduce phase of the
+// 2-shot all-reduce / rooted reduce, the reduce-scatter): those loads are non-temporal, so the
+// read-once inputs do not push out of the caches the reduced tiles the next phase re-reads.
+// (The staged protocols keep normal loads: their staging is written and re-read within a call.)
+#ifndef PDCC_IPC_ZC_NTL
+#define PDCC_IPC_ZC_NTL 1
+#endif
+template <DType DT, RedOp OP, int NSRC, int DEPTH, int NDST = 1, class Map>
+__device__ __forceinline__ void ipc_pipe_once(char* lds, const Map& m, int avg_div) {
+  pipe_run<DT, OP, NSRC, DEPTH, Map, NDST, false, PDCC_IPC_ZC_NTL != 0>(lds, m, avg_div);
+}
+
 // Register-staged engine (same Map contract): UNROLL tiles of NSRC vectors in
 // VGPRs per lane, no LDS. Kept for the A/B measurement against pipe_run.
 template <DType DT, RedOp OP, int NSRC, int UNROLL, class Map, bool NT = false, bool NTL = false>

@@ -351,7 +351,7 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
     {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
@@ -383,7 +383,7 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
     // reuse is guarded by the next call's arrival barrier).
     {
       const AllSrcMap<W> m{&v, 0, v.stg[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
+      ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
@@ -395,7 +395,7 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
     return;
   } else if (c.coll == IpcColl::REDUCE_SCATTER) {
     const AllSrcMap<W> m{&v, (size_t)me * c.zstride, (char*)c.out[0], c.bytes, b, G, nt};
-    ipc_pipe<DT, OP, W, D>(lds, m, c.avg_div);
+    ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
     tr.mark(5);
   }
   block_barrier<false>(v, ep + 3u);  // departure

@@ -55,13 +55,16 @@ def work(rank, size, n, kib, iters):
                 t0 = time.perf_counter()
                 fn()
                 torch.cuda.synchronize()
+                engine = b.last_algo()  # (before the host-transport MAX below records "shm")
                 t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 lat.append(t.item())
             res[f"{name}_{mode}_us"] = round(statistics.median(lat) * 1e6, 1)
             res[f"{name}_{mode}_collectives_per_call"] = round((_colls(b) - before) / iters, 2)
-            res[f"{name}_{mode}_engine"] = b.last_algo()
+            res[f"{name}_{mode}_engine"] = engine
         res[f"{name}_speedup"] = round(res[f"{name}_loop_us"] / res[f"{name}_coalesced_us"], 2)
+    res["autotune"] = [{k: e[k] for k in ("coll", "lo", "algo", "ref_us", "ipc_us", "staged_us")}
+                       for e in b.autotune_table()]
     return res
 
 

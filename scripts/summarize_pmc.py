@@ -32,42 +32,41 @@ def load(pass_dir):
     return out
 
 
-def short(k):
-    if "k1_" in k:
-        m = re.search(r"(k1_\w+)<[^,]*,[^,]*,\s*(\d)", k)
-        return m.group(1) if m else k[:40]
-    if "add" in k.lower() or "elementwise" in k.lower():
-        return "torch.add"
-    return k[:40]
+def label(k):
+    """(kernel label, source count) from a dispatch's kernel name; None for other kernels."""
+    m = re.search(r"k1_reduce_(lds|stream|regs)<\(pdcc::kern::DType\)\d+, \(pdcc::kern::RedOp\)\d+, (\d+)", k)
+    if m:
+        return f"k1 {m.group(1)}", int(m.group(2))
+    if "CUDAFunctor_add" in k or ("add" in k and "vectorized_elementwise" in k):
+        return "torch.add", 2
+    return None
 
 
 def main(root):
     passes = {t: load(os.path.join(root, t)) for t in ("rd", "wr", "fetch", "write")}
-    ids = sorted(set().union(*[set(p) for p in passes.values()]))
     mib = int(os.environ.get("PDCC_PMC_MIB", "512"))
-    # dispatch order of pmc_k1_big.py: (2 src: lds_ntl x3, stream_ntl x3), (8 src: same), torch.add x3
-    expect = [(2, "k1 lds_ntl")] * 3 + [(2, "k1 stream_ntl")] * 3 + [(8, "k1 lds_ntl")] * 3 + \
-             [(8, "k1 stream_ntl")] * 3 + [(2, "torch.add")] * 3
-    big = [d for d in ids if "reduce" in passes["rd"].get(d, {}).get("kernel", "") or
-           "add" in passes["rd"].get(d, {}).get("kernel", "").lower() or "elementwise" in
-           passes["rd"].get(d, {}).get("kernel", "").lower()]
     print("# PMC byte reconciliation: K1 and torch.add on 512 MiB fp32 sources (above the 256 MiB MALL)\n")
     print("`scripts/pmc_passes.sh` (four rocprofv3 --pmc passes, one counter set each) over "
-          "`scripts/pmc_k1_big.py`. MiB per dispatch; requests x their size = EA read bytes.\n")
-    print("| dispatch | kernel | nsrc | must read | RDREQ 32B/64B/128B (M) | EA read MiB | TCC_BUBBLE (M) "
-          "| FETCH_SIZE MiB | must write | WRREQ (M) 64B (M) | WRITE_SIZE MiB |")
+          "`scripts/pmc_k1_big.py`; MiB per dispatch. EA read MiB = 32 B x RDREQ_32B + 64 B x RDREQ_64B + "
+          "128 B x RDREQ_128B (the raw TCC->EA requests by size); FETCH_SIZE is rocprof's derived counter, "
+          "whose gfx950 formula counts 128-byte reads through TCC_BUBBLE.\n")
+    print("| dispatch | kernel | nsrc | must read | RDREQ 32B / 64B / 128B (M) | EA read MiB | TCC_BUBBLE | "
+          "FETCH_SIZE MiB | must write | WRREQ / WRREQ_64B (M) | WRITE_SIZE MiB |")
     print("|---|---|---|---|---|---|---|---|---|---|---|")
-    rows = [d for d in ids if d in passes["rd"]][-len(expect):] if len(big) < len(expect) else big[-len(expect):]
-    for d, (nsrc, label) in zip(rows, expect):
+    for d in sorted(passes["rd"]):
+        lab = label(passes["rd"][d].get("kernel", ""))
+        if lab is None:
+            continue
+        name, nsrc = lab
         rd, wr = passes["rd"].get(d, {}), passes["wr"].get(d, {})
-        r32, r64, r128 = (rd.get(f"TCC_EA0_RDREQ_{s}_sum", 0.0) for s in ("32B", "64B", "128B"))
+        r32, r64, r128 = (rd.get(f"TCC_EA0_RDREQ_{x}_sum", 0.0) for x in ("32B", "64B", "128B"))
         tot = rd.get("TCC_EA0_RDREQ_sum", 0.0)
         ea = (32 * r32 + 64 * r64 + 128 * r128 + 64 * max(0.0, tot - r32 - r64 - r128)) / MIB
         fetch = passes["fetch"].get(d, {}).get("FETCH_SIZE", 0.0) / 1024
         write = passes["write"].get(d, {}).get("WRITE_SIZE", 0.0) / 1024
-        print(f"| {d} | {label} | {nsrc} | {nsrc * mib} | {r32 / 1e6:.2f} / {r64 / 1e6:.2f} / {r128 / 1e6:.2f} | "
-              f"{ea:.1f} | {wr.get('TCC_BUBBLE_sum', 0.0) / 1e6:.2f} | {fetch:.1f} | {mib} | "
-              f"{wr.get('TCC_EA0_WRREQ_sum', 0.0) / 1e6:.2f} {wr.get('TCC_EA0_WRREQ_64B_sum', 0.0) / 1e6:.2f} | "
+        print(f"| {d} | {name} | {nsrc} | {nsrc * mib} | {r32 / 1e6:.2f} / {r64 / 1e6:.2f} / {r128 / 1e6:.2f} | "
+              f"{ea:.1f} | {wr.get('TCC_BUBBLE_sum', 0.0):.0f} | {fetch:.1f} | {mib} | "
+              f"{wr.get('TCC_EA0_WRREQ_sum', 0.0) / 1e6:.2f} / {wr.get('TCC_EA0_WRREQ_64B_sum', 0.0) / 1e6:.2f} | "
               f"{write:.1f} |")
 
 
