@@ -178,14 +178,21 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather_into_tensor_coalesc
     for (size_t i = 0; i < inputs.size(); ++i) pack_piece(inputs[i], fin, off[i], pk);
     if (gpu) run_copies(pk, current_stream(inputs[0].device().index()));
   }
-  // output i of rank r's block: bytes[i] at r * S + off[i] -> outputs[i][r * bytes[i]]
+  // output i of rank r's block: bytes[i] at r * S + off[i] -> outputs[i][r * bytes[i]] (outputs are
+  // contiguous: raw pointers, no per-piece tensor views -- 2 x 64 views cost more host time than the
+  // whole collective)
   auto co = std::make_shared<Coalesced>();
   co->members = outputs;
   for (size_t i = 0; i < outputs.size(); ++i) {
     if (bytes[i] == 0) continue;
     for (int r = 0; r < size_; ++r) {
-      at::Tensor dst = outputs[i].view(-1).narrow(0, (int64_t)r * inputs[i].numel(), inputs[i].numel());
-      unpack_piece(dst, fout, (size_t)r * S + off[i], *co);
+      if (gpu) {
+        co->unpack.push_back({byte_ptr(fout, (size_t)r * S + off[i]), byte_ptr(outputs[i], (size_t)r * bytes[i]),
+                              bytes[i]});
+      } else {
+        at::Tensor dst = outputs[i].view(-1).narrow(0, (int64_t)r * inputs[i].numel(), inputs[i].numel());
+        unpack_piece(dst, fout, (size_t)r * S + off[i], *co);
+      }
     }
   }
   std::vector<at::Tensor> outs;
@@ -240,6 +247,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter_tensor_coalesc
     c10::OptionalDeviceGuard g(outputs[0].device());
     for (size_t i = 0; i < inputs.size(); ++i) {
       if (bytes[i] == 0) continue;
+      if (gpu && inputs[i].is_contiguous()) {  // raw pointers (no per-piece tensor views)
+        for (int r = 0; r < size_; ++r)
+          pk.push_back({byte_ptr(inputs[i], (size_t)r * bytes[i]), byte_ptr(fin, (size_t)r * S + off[i]), bytes[i]});
+        continue;
+      }
       hold.push_back(inputs[i].reshape(-1));
       for (int r = 0; r < size_; ++r)
         pack_piece(hold.back().narrow(0, (int64_t)r * outputs[i].numel(), outputs[i].numel()), fin,

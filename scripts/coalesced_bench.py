@@ -33,18 +33,25 @@ def work(rank, size, n, kib, iters):
     outs = [torch.empty(m * size, device=d) for _ in range(n)]
     ins_rs = [torch.rand(m * size, device=d) for _ in range(n)]
     outs_rs = [torch.empty(m, device=d) for _ in range(n)]
+    pg = dist.distributed_c10d._get_default_group()
     cases = {
         "all_reduce": (lambda: [dist.all_reduce(x) for x in xs],
-                       lambda: _coal(d, lambda: [dist.all_reduce(x) for x in xs])),
+                       lambda: _coal(d, lambda: [dist.all_reduce(x) for x in xs]),
+                       lambda: dist.all_reduce_coalesced(xs)),
         "all_gather": (lambda: [dist.all_gather_into_tensor(o, x) for o, x in zip(outs, xs)],
-                       lambda: _coal(d, lambda: [dist.all_gather_into_tensor(o, x) for o, x in zip(outs, xs)])),
+                       lambda: _coal(d, lambda: [dist.all_gather_into_tensor(o, x) for o, x in zip(outs, xs)]),
+                       lambda: pg.allgather_into_tensor_coalesced(outs, xs).wait()),
         "reduce_scatter": (lambda: [dist.reduce_scatter_tensor(o, x) for o, x in zip(outs_rs, ins_rs)],
                            lambda: _coal(d, lambda: [dist.reduce_scatter_tensor(o, x)
-                                                     for o, x in zip(outs_rs, ins_rs)])),
+                                                     for o, x in zip(outs_rs, ins_rs)]),
+                           lambda: pg.reduce_scatter_tensor_coalesced(outs_rs, ins_rs,
+                                                                      dist.ReduceScatterOptions()).wait()),
     }
     res = {}
-    for name, (loop, coal) in cases.items():
-        for mode, fn in (("loop", loop), ("coalesced", coal)):
+    # modes: a Python loop of single collectives; torch's _coalescing_manager (records every op in
+    # Python, then ONE backend call); the backend's coalesced entry point called once from Python
+    for name, (loop, coal, direct) in cases.items():
+        for mode, fn in (("loop", loop), ("coalesced", coal), ("direct", direct)):
             fn()
             torch.cuda.synchronize()
             before = _colls(b)
@@ -63,6 +70,7 @@ def work(rank, size, n, kib, iters):
             res[f"{name}_{mode}_collectives_per_call"] = round((_colls(b) - before) / iters, 2)
             res[f"{name}_{mode}_engine"] = engine
         res[f"{name}_speedup"] = round(res[f"{name}_loop_us"] / res[f"{name}_coalesced_us"], 2)
+        res[f"{name}_speedup_direct"] = round(res[f"{name}_loop_us"] / res[f"{name}_direct_us"], 2)
     res["autotune"] = [{k: e[k] for k in ("coll", "lo", "algo", "ref_us", "ipc_us", "staged_us")}
                        for e in b.autotune_table()]
     return res

@@ -1701,9 +1701,9 @@ def async_grid_probe(rank, size, device="cuda", calls=6):
     b = be.native_backend(None, "cuda")
     ok = True
 
-    def capped():
+    def capped():  # (0 before the group's IPC communicator exists)
         m = re.search(r"async_capped=(\d+)", b.describe())
-        return int(m.group(1)) if m else -1
+        return int(m.group(1)) if m else 0
 
     res = {}
     for n in (1000, (4 << 20) // 4 + 7):  # LL and zero-copy 2-shot (+ staged rest)

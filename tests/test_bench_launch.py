@@ -60,3 +60,18 @@ def test_bench_failing_rank_propagates():
     r = _run(["--gpus", "2", "--bytes", "4096", "--steps", "2", "--warmup", "1"], {"PDCC_FAULT": "1:3:exit"})
     assert r.returncode != 0
     assert "rank 1 exited" in r.stderr
+
+
+def test_vs_torch_nccl_ratios():
+    # verdict r3 Next #3: torch's ProcessGroupNCCL p50 / ours per row (> 1: this library is faster)
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    ours = {"all_reduce_1GiB": {"p50_ms": 2.0}, "reduce_1GiB": {"p50_ms": 4.0}}
+    theirs = {"rows": {"all_reduce_1GiB": {"p50_ms": 3.0}, "reduce_1GiB": {"p50_ms": 2.0}, "extra": {"p50_ms": 1}}}
+    assert bench.vs_torch_nccl(ours, theirs) == {"all_reduce_1GiB": 1.5, "reduce_1GiB": 0.5}
+    if not bench.SMALL:
+        assert bench._vs_torch_nccl_headline({"torch_nccl": theirs}, 0.002) == 1.5
+    assert bench._vs_torch_nccl_headline({"torch_nccl": {"skipped": "x"}}, 0.002) is None
