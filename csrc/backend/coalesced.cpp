@@ -62,6 +62,15 @@ void unpack_piece(const at::Tensor& dst, const at::Tensor& flat, size_t off, Coa
                          flat.narrow(0, (int64_t)off, (int64_t)dst.nbytes()).view(dst.scalar_type()).view(dst.sizes()));
 }
 
+// torch's _coalescing_manager calls the coalesced entry points between start- and endCoalescing;
+// the one collective they run is issued at once, so it may be autotuned like any other call
+struct IssueNow {
+  bool& flag;
+  const bool saved;
+  explicit IssueNow(bool& f) : flag(f), saved(f) { flag = false; }
+  ~IssueNow() { flag = saved; }
+};
+
 void run_copies(const std::vector<kern::CopyDesc>& d, hipStream_t s) {
   if (!d.empty()) PDCC_HIP(kern::multi_copy(d.data(), (int)d.size(), s));
 }
@@ -128,6 +137,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allreduce_coalesced(std::vect
     for (size_t i = 0; i < tensors.size(); ++i) unpack_piece(tensors[i], flat, off[i], *co);
     std::vector<at::Tensor> one{typed};
     before_op(Coll::ALLREDUCE, one, -1);
+    IssueNow now(coalescing_);
     auto w = gpu_allreduce(typed, opts.reduceOp.op_, -1, false, eff_timeout(opts.timeout), co);
     record_setup("coalesced/allreduce x" + std::to_string(tensors.size()), t0);
     return w;
@@ -200,6 +210,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::allgather_into_tensor_coalesc
   std::vector<at::Tensor> one{fin};
   before_op(Coll::ALLGATHER, one, -1);
   if (gpu) {
+    IssueNow now(coalescing_);
     auto w = gpu_allgather(outs, fin, -1, false, eff_timeout(opts.timeout), co);
     record_setup("coalesced/allgather x" + std::to_string(inputs.size()), t0);
     return w;
@@ -269,6 +280,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::reduce_scatter_tensor_coalesc
   std::vector<at::Tensor> one{tout};
   before_op(Coll::REDUCE_SCATTER, one, -1);
   if (gpu) {
+    IssueNow now(coalescing_);
     auto w = gpu_reduce_scatter(tout, ins, opts.reduceOp.op_, eff_timeout(opts.timeout), co);
     record_setup("coalesced/reduce_scatter x" + std::to_string(inputs.size()), t0);
     return w;

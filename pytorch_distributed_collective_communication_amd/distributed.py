@@ -54,3 +54,27 @@ def is_mi355x_available() -> bool:
     from . import native_available
 
     return native_available()
+
+
+def _pg(group):
+    return group if group is not None else _td.distributed_c10d._get_default_group()
+
+
+def all_gather_into_tensor_coalesced(outputs, inputs, group=None, async_op=False):
+    """Every ``inputs[i]`` gathered into ``outputs[i]`` (``world x`` its size) as ONE collective:
+    the backend packs the members, runs one all-gather and unpacks (csrc/backend/coalesced.cpp).
+    The same call torch's ``_coalescing_manager`` makes, without recording each member in Python."""
+    work = _pg(group).allgather_into_tensor_coalesced(list(outputs), list(inputs))
+    if async_op:
+        return work
+    work.wait()
+
+
+def reduce_scatter_tensor_coalesced(outputs, inputs, op=ReduceOp.SUM, group=None, async_op=False):
+    """Chunk ``rank`` of every ``inputs[i]``, reduced over the group, into ``outputs[i]`` -- ONE collective."""
+    opts = _td.ReduceScatterOptions()
+    opts.reduceOp = op
+    work = _pg(group).reduce_scatter_tensor_coalesced(list(outputs), list(inputs), opts)
+    if async_op:
+        return work
+    work.wait()

@@ -145,3 +145,8 @@ def test_coalesced_collectives_are_one_operation(world):
         assert r["allgather_ok"] and r["reduce_scatter_ok"], r
         assert r["allreduce_collectives"] == 1 and r["allreduce_coalesced_api_collectives"] == 1, r
         assert r["allgather_collectives"] == 1 and r["reduce_scatter_collectives"] == 1, r
+
+
+def test_coalesced_direct_entry_points():
+    for r in launch(W.coalesced_direct, 3, args=("cpu",)):
+        assert r == {"ag": True, "rs": True}, r
