@@ -141,6 +141,7 @@ Config Config::from_env() {
   c.a2a_list_agree = env_bool("PDCC_A2A_LIST_AGREE", c.a2a_list_agree);
   if (const char* it = env("PDCC_RCCL_INIT_TIMEOUT_S")) c.rccl_init_timeout_ms = (int64_t)(std::atof(it) * 1000.0);
   c.rccl_init_timeout_ms = std::max<int64_t>(1, c.rccl_init_timeout_ms);
+  c.rccl_nonblocking = env_bool("PDCC_RCCL_NONBLOCKING", c.rccl_nonblocking);
   c.rccl_min_ctas = env_int("PDCC_RCCL_MIN_CTAS", c.rccl_min_ctas);
   c.rccl_max_ctas = env_int("PDCC_RCCL_MAX_CTAS", c.rccl_max_ctas);
   c.rccl_wide_ctas = std::max(0, env_int("PDCC_RCCL_WIDE_CTAS", c.rccl_wide_ctas));
@@ -178,7 +179,7 @@ std::string Config::describe() const {
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
     << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
-    << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms
+    << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms << " rccl_nonblocking=" << rccl_nonblocking
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")
     << " split_share=" << rccl_split_share << " list_gather=" << (list_gather_p2p ? "p2p" : "staged")
     << " a2a_list_agree=" << a2a_list_agree

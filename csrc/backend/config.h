@@ -114,6 +114,7 @@ struct Config {
   // polled, so a peer that dies or never arrives fails the group within this bound
   // instead of hanging every other rank (the reference's Gloo surfaces it in ~0.2 s).
   int64_t rccl_init_timeout_ms = 300000;   // PDCC_RCCL_INIT_TIMEOUT_S (seconds)
+  bool rccl_nonblocking = true;            // PDCC_RCCL_NONBLOCKING=0: blocking creation, no deadline
   int rccl_min_ctas = -1;                  // PDCC_RCCL_MIN_CTAS
   int rccl_max_ctas = -1;                  // PDCC_RCCL_MAX_CTAS
   // Wide RCCL: a child communicator (ncclCommSplit, own resources) with at least this many

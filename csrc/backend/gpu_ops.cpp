@@ -1058,7 +1058,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_p2p(at::Tensor& t, int pe
         // self-contained (copies only): the thread may outlive a group destroyed meanwhile
         const int lo = std::min(rank_, peer), hi = std::max(rank_, peer);
         std::thread([pc, store = store_, key = "pdcc/p2p/" + std::to_string(lo) + ":" + std::to_string(hi),
-                     prank = rank_ == lo ? 0 : 1, dev = ds.device, pi, init_ms = rccl_opts().init_timeout_ms] {
+                     prank = rank_ == lo ? 0 : 1, dev = ds.device, pi,
+                     init_ms = cfg_.rccl_nonblocking ? rccl_opts().init_timeout_ms : int64_t{0}] {
           pair_builder(pc, store, key, prank, dev, pi, init_ms);
         }).detach();
       }
@@ -1090,6 +1091,7 @@ void ProcessGroupMI355X::pair_builder(std::shared_ptr<PairChan> pc, c10::intrusi
     const auto t0 = std::chrono::steady_clock::now();
     RcclOpts o;
     o.init_timeout_ms = init_ms;  // the peer may never post its side: bounded
+    o.nonblocking = init_ms > 0;
     auto c = std::make_shared<RcclComm>(store, key, prank, 2, dev, o);
     std::lock_guard<std::mutex> lk(pc->mu);
     pc->comm = c;

@@ -187,6 +187,7 @@ RcclOpts ProcessGroupMI355X::rccl_opts() const {
   o.max_ctas = cfg_.rccl_max_ctas;
   o.split_share = cfg_.rccl_split_share ? 1 : 0;
   o.init_timeout_ms = std::max<int64_t>(1, std::min<int64_t>(cfg_.rccl_init_timeout_ms, timeout_.count()));
+  o.nonblocking = cfg_.rccl_nonblocking;
   return o;
 }
 

@@ -29,7 +29,7 @@ struct DeviceGuard {
 
 ncclConfig_t make_config(const RcclOpts& o, bool for_split) {
   ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = 0;  // creation is polled against a deadline (wait_ready)
+  cfg.blocking = o.nonblocking ? 0 : 1;  // non-blocking: creation is polled against a deadline (wait_ready)
   if (o.min_ctas > 0) cfg.minCTAs = o.min_ctas;
   if (o.max_ctas > 0) cfg.maxCTAs = o.max_ctas;
   if (for_split) cfg.splitShare = o.split_share ? 1 : 0;

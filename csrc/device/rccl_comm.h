@@ -56,6 +56,7 @@ struct RcclOpts {
   // non-blocking (ncclConfig_t.blocking = 0) and polled; past the deadline the half-built
   // communicator is aborted and the constructor throws (a peer died or never joined)
   int64_t init_timeout_ms = 300000;
+  bool nonblocking = true;  // PDCC_RCCL_NONBLOCKING=0: RCCL's blocking creation (no deadline), as before round 4
   bool any() const { return min_ctas > 0 || max_ctas > 0; }
 };
 

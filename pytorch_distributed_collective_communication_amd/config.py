@@ -29,6 +29,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_AUTOTUNE_SPIN_MS | 10000 | spin bound of IPC runs during tuning; a timeout drops IPC for that key and keeps the group healthy |
 | PDCC_AUTOTUNE_FILE | "" | persisted decisions: keys with a line in this file (same topology signature on every rank) take the recorded engine without a race; rank 0 appends every new race's verdict |
 | PDCC_RCCL_INIT_TIMEOUT_S | 300 | deadline of one RCCL communicator creation (non-blocking init / split, polled; capped by the group timeout): a peer that never joins fails the group with a clear error, later calls fail at once |
+| PDCC_RCCL_NONBLOCKING | 1 | create RCCL communicators non-blocking (polled against the deadline above); 0: RCCL's blocking creation |
 | PDCC_RCCL_MIN_CTAS / _MAX_CTAS | -1 / -1 | RCCL channel (CTA) bounds via ``ncclCommInitRankConfig``; -1 leaves RCCL's topology tuner in charge |
 | PDCC_RCCL_GROUP_COMM | share | groups with the same members as a live communicator: share it, split from it (ncclCommSplit) or init a fresh one |
 | PDCC_RCCL_SPLIT_SHARE | 1 | ncclCommSplit children share the parent's resources |
@@ -102,6 +103,7 @@ class Config:
     autotune_spin_ms: int = 10000
     autotune_file: str = ""
     rccl_init_timeout_s: int = 300
+    rccl_nonblocking: bool = True
     rccl_min_ctas: int = -1
     rccl_max_ctas: int = -1
     rccl_wide_ctas: int = 112
@@ -132,7 +134,8 @@ _ENV = {
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC",
-    "ipc_zx": "PDCC_IPC_ZX", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S", "autotune": "PDCC_AUTOTUNE",
+    "ipc_zx": "PDCC_IPC_ZX", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S",
+    "rccl_nonblocking": "PDCC_RCCL_NONBLOCKING", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",
     "autotune_colls": "PDCC_AUTOTUNE_COLLS", "autotune_spin_ms": "PDCC_AUTOTUNE_SPIN_MS",

@@ -32,6 +32,7 @@ import argparse
 import datetime
 import json
 import os
+import shutil
 import signal
 import socket
 import statistics
@@ -181,6 +182,7 @@ def sweep(store, rank: int, world: int, local_rank: int, nbytes: int = 1 << 30, 
         out_rec = {"points": results, "winner": best, "applied_env": env, "min_gain": 0.05,
                    "bytes": nbytes, "iters": iters, "elapsed_s": round(time.time() - t_start, 1)}
         store.set(f"{key}/record", json.dumps(out_rec))
+        shutil.rmtree(tmp, ignore_errors=True)
     store.wait([f"{key}/record"], wait)
     out_rec = json.loads(store.get(f"{key}/record"))
     return out_rec, out_rec.get("applied_env") or {}
@@ -206,6 +208,7 @@ def sweep_local(world: int, nbytes: int = 1 << 30, budget_s: float = 300.0, poin
             rec["stderr_tail"] = next((t for t in tails if t), "")
         results[name] = rec
     best, env = _decide(results)
+    shutil.rmtree(tmp, ignore_errors=True)
     return {"points": results, "winner": best, "applied_env": env, "bytes": nbytes, "iters": iters,
             "elapsed_s": round(time.time() - t_start, 1)}
 
