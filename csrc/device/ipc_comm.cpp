@@ -147,7 +147,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       const long n = std::atol(tr);
       if (n > 0) {
         trace_cap_ = (uint32_t)std::min<long>(n, 1 << 20);
-        const size_t tb = (size_t)trace_cap_ * kern::kTraceWords * sizeof(uint64_t);
+        const size_t tb = (size_t)trace_cap_ * kern::kTraceRecWords * sizeof(uint64_t);
         PDCC_HIP(hipHostMalloc(reinterpret_cast<void**>(&trace_host_), tb, hipHostMallocMapped | hipHostMallocCoherent));
         std::memset(trace_host_, 0, tb);
         PDCC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&trace_dev_), trace_host_, 0));
@@ -703,9 +703,9 @@ void IpcComm::clear_error() {
 std::vector<std::vector<uint64_t>> IpcComm::trace_records() const {
   std::vector<std::vector<uint64_t>> out;
   for (uint32_t i = 0; trace_host_ && i < trace_cap_; ++i) {
-    const volatile uint64_t* r = trace_host_ + (size_t)i * kern::kTraceWords;
+    const volatile uint64_t* r = trace_host_ + (size_t)i * kern::kTraceRecWords;
     if (r[1] == 0) continue;  // never written
-    out.emplace_back(r, r + kern::kTraceWords);
+    out.emplace_back(r, r + kern::kTraceRecWords);
   }
   std::sort(out.begin(), out.end(), [](const auto& a, const auto& b) { return a[1] < b[1]; });
   return out;

@@ -89,7 +89,7 @@ class IpcComm {
   void abort();
 
   // PDCC_IPC_TRACE=N: kernels record per-phase device timestamps of block 0 into a
-  // host-mapped ring of N records (kern::kTraceWords u64 each); copies of the valid ones
+  // host-mapped ring of N records (kern::kTraceRecWords u64 each: header + per-block stamps); copies of the valid ones
   std::vector<std::vector<uint64_t>> trace_records() const;
   bool shared_device() const { return shared_device_; }
   int world() const { return world_; }

@@ -431,10 +431,10 @@ __device__ __forceinline__ uint32_t block_seq(const V& v) {
 }
 
 // ----------------------------------------------------------------------------
-// Phase trace (PDCC_IPC_TRACE): block 0 / thread 0 keeps timestamps in registers
-// and writes the record once, when the kernel body returns (finish(); no extra
-// memory traffic inside the protocol).
-// The record lives in LDS (64 B per workgroup): a trace object in registers gets
+// Phase trace (PDCC_IPC_TRACE): thread 0 of every block keeps timestamps and writes
+// them once, when the kernel body returns (finish(); no extra memory traffic inside
+// the protocol): block 0 the record header, every block its phase-1 and exit stamps.
+// The stamps live in LDS (96 B per workgroup): a trace object in registers gets
 // demoted to scratch memory once it crosses the kernel body's many exit paths.
 struct PhaseTrace {
   const bool on;
@@ -443,7 +443,7 @@ struct PhaseTrace {
     return s;
   }
   __device__ __forceinline__ explicit PhaseTrace(const kern::IpcView& view)
-      : on(view.trace != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+      : on(view.trace != nullptr && threadIdx.x == 0) {
     if (on) {
 #pragma unroll
       for (int k = 0; k < kern::kTraceWords; ++k) slots()[k] = 0;
@@ -460,9 +460,15 @@ struct PhaseTrace {
     if (!on) return;
     uint64_t* t = slots();
     t[7] = __builtin_amdgcn_s_memrealtime();
-    uint64_t* r = view.trace + (size_t)(t[0] % view.trace_cap) * kern::kTraceWords;
+    uint64_t* r = view.trace + (size_t)(t[0] % view.trace_cap) * kern::kTraceRecWords;
+    if (blockIdx.x == 0) {
 #pragma unroll
-    for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];
+      for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];
+    }
+    if (blockIdx.x < (unsigned)kern::kTraceBlocks) {
+      r[kern::kTraceWords + blockIdx.x] = t[5];
+      r[kern::kTraceWords + kern::kTraceBlocks + blockIdx.x] = t[7];
+    }
   }
 };
 

@@ -129,6 +129,12 @@ using IpcView = IpcViewT<RawPtr>;
 // [8] every rank's record in, [9] mapping lookup done, [10] every vote in, [11] verdict published.
 // Record `seq % trace_cap`.
 constexpr int kTraceWords = 12;
+// After the header, per block b < kTraceBlocks: [kTraceWords + b] the block's first pull /
+// reduce done ([5]), [kTraceWords + kTraceBlocks + b] its exit ([7]) -- how far the slowest
+// block trails block 0. A block files into the record of ITS call number, so the per-block
+// stamps line up with block 0's header when every call runs at the same grid.
+constexpr int kTraceBlocks = 256;
+constexpr int kTraceRecWords = kTraceWords + 2 * kTraceBlocks;
 
 enum class IpcColl : int32_t {
   ALLREDUCE_1SHOT = 0,   // stage, barrier, every rank reduces everything from all peers

@@ -63,7 +63,7 @@ def work(rank, size, mib, iters):
     phases = {"entry_to_arrival": ph(1, 2), "arrival_to_data_barrier": ph(2, 4), "stage_or_gate": ph(2, 3),
               "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7)}
     out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
-           "phases_us": phases, "records": len(recs)}
+           "phases_us": phases, "records": len(recs), "blocks_us": blocks(recs)}
     # K1 at the same total workgroup budget: rank 0 alone, the others wait
     dist.barrier()
     if rank == 0:
@@ -83,6 +83,35 @@ def work(rank, size, mib, iters):
         out["k1"] = k1
     dist.barrier()
     return out
+
+
+HDR, NB = 12, 256  # kern::kTraceWords, kern::kTraceBlocks
+
+
+def blocks(recs):
+    """Every block against block 0 (per-block stamps after the header, measured from block
+    0's entry): median over calls of the median / slowest block's phase-1 end and exit."""
+    p1_med, p1_max, ex_med, ex_max, n = [], [], [], [], 0
+    for r in recs:
+        if len(r) < HDR + 2 * NB:
+            return None
+        t0 = r[1]
+        p1 = [(x - t0) / 100.0 for x in r[HDR:HDR + NB] if x >= t0]
+        ex = [(x - t0) / 100.0 for x in r[HDR + NB:HDR + 2 * NB] if x >= t0]
+        if not ex:
+            continue
+        n = max(n, len(ex))
+        ex_med.append(statistics.median(ex))
+        ex_max.append(max(ex))
+        if p1:
+            p1_med.append(statistics.median(p1))
+            p1_max.append(max(p1))
+
+    def med(v):
+        return round(statistics.median(v), 1) if v else None
+
+    return {"blocks": n, "phase1_done_median_block": med(p1_med), "phase1_done_slowest_block": med(p1_max),
+            "exit_median_block": med(ex_med), "exit_slowest_block": med(ex_max)}
 
 
 def main():
