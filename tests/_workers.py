@@ -1744,3 +1744,35 @@ def coalesced_direct(rank, size, device="cpu"):
     ok_rs = all(torch.equal(rout[i].cpu(), torch.arange(rank * (2 + i), (rank + 1) * (2 + i), dtype=torch.float32)
                             + (size - 1)) for i in range(5))
     return {"ag": ok_ag, "rs": ok_rs}
+
+
+def phase_trace_probe(rank, size, device="cuda", calls=6, mib=8):
+    """PDCC_IPC_TRACE: block 0's header stamps are ordered and every traced block of a
+    2-shot all_reduce files its phase-1 and exit stamps into the same record."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    x = torch.empty((mib << 20) // 4, device=d)
+    ok = True
+    for _ in range(calls):
+        x.fill_(float(rank + 1))
+        dist.all_reduce(x)
+        ok = ok and bool(torch.all(x == size * (size + 1) / 2))
+    torch.cuda.synchronize()
+    HDR, NB = 12, 256
+    recs = [r for r in b.ipc_trace() if r[1] and r[7]]
+    out = {"ok": ok, "engine": b.last_algo(), "records": len(recs), "rec_words": len(recs[-1]) if recs else 0}
+    if recs:
+        r = recs[-1]
+        out["header_ordered"] = r[1] <= r[2] <= r[4] <= r[5] <= r[6] <= r[7]
+        ex = [v for v in r[HDR + NB:HDR + 2 * NB] if v >= r[1]]
+        p1 = [v for v in r[HDR:HDR + NB] if v >= r[1]]
+        out["blocks_exit"] = len(ex)
+        out["blocks_phase1"] = len(p1)
+        out["slowest_exit_after_block0_us"] = (max(ex) - r[7]) / 100.0 if ex else None
+        out["phase1_before_exit"] = all(a <= e for a, e in zip(r[HDR:HDR + NB], r[HDR + NB:HDR + 2 * NB]) if a)
+    return out

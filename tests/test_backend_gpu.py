@@ -559,6 +559,18 @@ def test_zero_copy_device_exchange_epoch_wraps():
         assert r["fast"] >= 30, (r["fast"], r["host"], r["desc"])
 
 
+def test_phase_trace_records_every_block():
+    # PDCC_IPC_TRACE: block 0's header plus every block's phase-1 / exit stamps (how far the
+    # slowest block trails block 0 -- scripts/ipc_phase_trace.py blocks_us)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_TRACE": "16", "PDCC_AUTOTUNE": "0"}
+    for r in _gpu_launch(W.phase_trace_probe, 2, env=env, timeout_s=120):
+        assert r["ok"] and r["records"] >= 1 and r["rec_words"] == 12 + 2 * 256, r
+        assert r["engine"].startswith("ipc_2shot"), r
+        assert r["header_ordered"] and r["phase1_before_exit"], r
+        assert r["blocks_exit"] >= 2 and r["blocks_phase1"] == r["blocks_exit"], r  # 256 / W blocks share one GPU
+        assert r["slowest_exit_after_block0_us"] is not None and r["slowest_exit_after_block0_us"] < 1e5, r
+
+
 def test_async_collectives_take_the_capped_grid():
     # verdict r3 Next #4: PDCC_IPC_ASYNC_GRID caps the IPC / LL launches of async_op=True
     # collectives (overlapped with compute); synchronous ones keep the full grid
