@@ -521,6 +521,23 @@ def test_rccl_communicator_creation_is_bounded():
     assert "PDCC_TEST_RCCL_INIT_SKIP" in r1["first"], r1
 
 
+def test_rccl_env_sweep_children_run_on_the_gpu(monkeypatch):
+    # the RCCL buffer/protocol pre-sweep's child ranks (utils/rccl_env.py) on a real GPU: one
+    # rank (the box has one GPU; RCCL forced on its 1-rank communicator), a 64 MiB all_reduce
+    # per point inside a 40 s budget -- the default point must run, on RCCL, with its p50
+    from pytorch_distributed_collective_communication_amd.utils import rccl_env
+
+    monkeypatch.setenv("PDCC_WORLD1_LOCAL", "0")
+    rec = rccl_env.sweep_local(1, nbytes=64 << 20, budget_s=40.0, point_timeout_s=30.0, iters=3)
+    first = rec["points"][rccl_env.points()[0][0]]
+    assert isinstance(first, dict) and first["ok"], rec
+    assert first["engine"].startswith("rccl") and first["p50_ms"] > 0, first
+    assert rec["elapsed_s"] < 90, rec
+    ran = [v for v in rec["points"].values() if isinstance(v, dict)]
+    assert all(v["ok"] for v in ran), rec
+    assert any(v.get("env", {}).get("NCCL_BUFFSIZE") for v in ran[1:]) or len(ran) == 1, rec
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_coalesced_collectives_one_launch(world):
     # verdict r3 Next #5: 64 ragged members per coalesced call -> ONE collective (K2 pack, one
