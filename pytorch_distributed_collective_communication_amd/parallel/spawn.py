@@ -147,6 +147,10 @@ def launch(
                 p.terminate()
         for p in procs:
             p.join(timeout=10)
+        for p in procs:  # a rank that ignores SIGTERM (stuck in a GPU wait, or a profiler's handler
+            if p.is_alive():  # chained in front of it) would block interpreter exit in its join
+                p.kill()
+                p.join(timeout=10)
         msg = "\n".join(f"rank {r}: {e}" for r, e in sorted(errors.items()))
         raise RuntimeError(f"distributed run failed:\n{msg}")
     for p in procs:

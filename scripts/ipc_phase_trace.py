@@ -63,7 +63,7 @@ def work(rank, size, mib, iters):
     phases = {"entry_to_arrival": ph(1, 2), "arrival_to_data_barrier": ph(2, 4), "stage_or_gate": ph(2, 3),
               "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7)}
     out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
-           "phases_us": phases, "records": len(recs), "blocks_us": blocks(recs)}
+           "phases_us": phases, "records": len(recs), "blocks_us": block_spread(recs)}
     # K1 at the same total workgroup budget: rank 0 alone, the others wait
     dist.barrier()
     if rank == 0:
@@ -88,7 +88,7 @@ def work(rank, size, mib, iters):
 HDR, NB = 12, 256  # kern::kTraceWords, kern::kTraceBlocks
 
 
-def blocks(recs):
+def block_spread(recs):
     """Every block against block 0 (per-block stamps after the header, measured from block
     0's entry): median over calls of the median / slowest block's phase-1 end and exit."""
     p1_med, p1_max, ex_med, ex_max, n = [], [], [], [], 0
