@@ -337,7 +337,13 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
     ++async_capped_;
   }
   DeviceScope ds(device_);
-  PDCC_HIP(kern::ipc_launch(v, call, stream));
+  if (!v.trace) {
+    PDCC_HIP(kern::ipc_launch(v, call, stream));
+    return;
+  }
+  kern::IpcView tv = v;  // PDCC_IPC_TRACE: every block of this launch files into one record
+  tv.trace_slot = seq_ % trace_cap_;
+  PDCC_HIP(kern::ipc_launch(tv, call, stream));
 }
 
 // ------------------------------------------------------------------ zero copy

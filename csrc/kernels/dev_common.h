@@ -460,7 +460,7 @@ struct PhaseTrace {
     if (!on) return;
     uint64_t* t = slots();
     t[7] = __builtin_amdgcn_s_memrealtime();
-    uint64_t* r = view.trace + (size_t)(t[0] % view.trace_cap) * kern::kTraceRecWords;
+    uint64_t* r = view.trace + (size_t)view.trace_slot * kern::kTraceRecWords;
     if (blockIdx.x == 0) {
 #pragma unroll
       for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];

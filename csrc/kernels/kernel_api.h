@@ -119,6 +119,7 @@ struct IpcViewT {
   uint64_t timeout_ticks;        // s_memrealtime ticks (100 MHz) before a spin gives up
   P<uint64_t> trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
   uint32_t trace_cap;            // records in the ring
+  uint32_t trace_slot;           // this launch's record (the host's launch counter % trace_cap)
 };
 using IpcView = IpcViewT<RawPtr>;
 
@@ -127,12 +128,11 @@ using IpcView = IpcViewT<RawPtr>;
 // staged (a gated launch: its gate passed), [4] data barrier passed, [5] first pull / reduce done, [6] second data
 // barrier passed (2-shot), [7] exit; a gated zero-copy launch's device-side exchange (block 0):
 // [8] every rank's record in, [9] mapping lookup done, [10] every vote in, [11] verdict published.
-// Record `seq % trace_cap`.
+// Record `trace_slot` (one per launch, whatever the grid).
 constexpr int kTraceWords = 12;
 // After the header, per block b < kTraceBlocks: [kTraceWords + b] the block's first pull /
 // reduce done ([5]), [kTraceWords + kTraceBlocks + b] its exit ([7]) -- how far the slowest
-// block trails block 0. A block files into the record of ITS call number, so the per-block
-// stamps line up with block 0's header when every call runs at the same grid.
+// block trails block 0.
 constexpr int kTraceBlocks = 256;
 constexpr int kTraceRecWords = kTraceWords + 2 * kTraceBlocks;
 
