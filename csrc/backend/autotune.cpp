@@ -39,6 +39,10 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
       bytes > cfg_.ipc_1shot_max)
     v.push_back(Algo::IPC_PUSH);
+  // the dynamic 2-shot all-reduce (zero-copy sizes): work items claimed per workgroup
+  if (c == Coll::ALLREDUCE && cfg_.ipc_dyn && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
+      bytes > cfg_.ipc_1shot_max)
+    v.push_back(Algo::IPC_DYN);
   return v;
 }
 
@@ -200,6 +204,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
       (cands[k] == Algo::IPC          ? te.ipc_us
        : cands[k] == Algo::IPC_WIDE   ? te.ipc_wide_us
        : cands[k] == Algo::IPC_STAGED ? te.staged_us
+       : cands[k] == Algo::IPC_DYN    ? te.dyn_us
                                       : te.push_us) = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
     } else if (cands[k] == Algo::RCCL_WIDE) {
@@ -218,9 +223,9 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   if (cfg_.log_level >= 1 && rank_ == 0)
     fprintf(stderr,
             "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us,"
-            " ipc_staged %.1f us%s (%d runs each) -> %s\n",
+            " ipc_staged %.1f us, ipc_dyn %.1f us%s (%d runs each) -> %s\n",
             coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us,
-            te.ipc_wide_us, te.push_us, te.staged_us,
+            te.ipc_wide_us, te.push_us, te.staged_us, te.dyn_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -270,10 +275,11 @@ void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, con
   }
   flock(fileno(f), LOCK_EX);
   std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
-               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f\n",
+               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f, ipc_dyn %.1f\n",
                tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
                algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref), (size_t)1 << std::get<3>(key),
-               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us);
+               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us,
+               e.dyn_us);
   std::fflush(f);
   flock(fileno(f), LOCK_UN);
   std::fclose(f);
@@ -297,6 +303,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.push_us = e.push_us;
     r.ipc_wide_us = e.ipc_wide_us;
     r.staged_us = e.staged_us;
+    r.dyn_us = e.dyn_us;
     r.wide_us = e.wide_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);

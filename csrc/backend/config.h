@@ -17,9 +17,13 @@ namespace pdcc {
 // IPC_STAGED: the IPC protocols with zero copy off for the call (inputs copied into the
 // registered staging buffer): raced against IPC (zero copy) for keys from ipc_zc_min, so the
 // zero-copy / staging crossover is measured per node instead of fixed.
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE, IPC_STAGED };
+// IPC_DYN: the zero-copy 2-shot all-reduce with work items claimed dynamically and per-chunk
+// ready words instead of fixed tile ranges and a block-pairwise barrier (kern::kDynOffset),
+// an autotuner candidate next to IPC for zero-copy all_reduce keys.
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE, IPC_STAGED, IPC_DYN };
 inline bool is_ipc(Algo a) {
-  return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE || a == Algo::IPC_STAGED;
+  return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE || a == Algo::IPC_STAGED ||
+         a == Algo::IPC_DYN;
 }
 inline bool is_rccl(Algo a) { return a == Algo::RCCL || a == Algo::RCCL_WIDE; }
 
@@ -40,6 +44,7 @@ struct Config {
   // The autotuner also races the push all-reduce (owners receive their tiles by remote writes,
   // reduce locally and write the result into every rank's tensor) for zero-copy sizes.
   bool ipc_push = true;                    // PDCC_IPC_PUSH
+  bool ipc_dyn = true;                     // PDCC_IPC_DYN: race the dynamic 2-shot all-reduce (IPC_DYN)
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
   // All-reduces up to this size (<= 256 KiB, kern::kLLMaxBytes) use the LL protocol: every
   // rank pushes flag-tagged 8-byte words into its peers' signal areas and polls its own --

@@ -34,6 +34,8 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
       return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_WIDE && ipc_can)  // only all_reduce races the wide grid
       return c == Coll::ALLREDUCE ? Algo::IPC_WIDE : Algo::IPC;
+    if (cfg_.force_algo == Algo::IPC_DYN && ipc_can)  // only the (zero-copy) all_reduce has it
+      return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_DYN : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_STAGED && ipc_can) return Algo::IPC_STAGED;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
@@ -156,6 +158,7 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
   if (body == call.bytes) return;
   kern::IpcCall rest = call;
   if (rest.coll == kern::IpcColl::ALLREDUCE_PUSH) rest.coll = kern::IpcColl::ALLREDUCE_2SHOT;  // zero-copy only
+  rest.dyn = 0;                                                                                 // (likewise)
   rest.bytes = call.bytes - body;
   for (int k = 0; k < kern::kMaxRanks; ++k) {
     if (call.in[k]) rest.in[k] = static_cast<const char*>(call.in[k]) + body;
@@ -329,6 +332,7 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
+    if (a == Algo::IPC_DYN && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.dyn = 1;  // (zero-copy runs only)
     // small (all-)reduce: flag-tagged pushes, no staging copy, no barrier
     if (ds.ll_ok && bytes_in_ll_range(w.nbytes()))
       c.coll = rooted ? kern::IpcColl::REDUCE_LL : kern::IpcColl::ALLREDUCE_LL;
@@ -692,6 +696,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
                              : one_shot                         ? "ipc_1shot"
                              : a == Algo::IPC_PUSH && !rooted ? "ipc_push"
                              : a == Algo::IPC_WIDE            ? "ipc_2shot_wide"
+                             : a == Algo::IPC_DYN && !rooted  ? "ipc_2shot_dyn"
                                                               : "ipc_2shot")
                           : a == Algo::RCCL_WIDE ? "rccl_wide" : "rccl", bytes, t0);
   hp_.lap(HostStage::RECORD);

@@ -742,7 +742,8 @@ void ProcessGroupMI355X::set_algo(const std::string& a) {
   else if (a == "rccl_wide") cfg_.force_algo = Algo::RCCL_WIDE;
   else if (a == "ipc_wide") cfg_.force_algo = Algo::IPC_WIDE;
   else if (a == "ipc_staged") cfg_.force_algo = Algo::IPC_STAGED;
-  else TORCH_CHECK(false, "set_algo: expected auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|host, got ", a);
+  else if (a == "ipc_dyn") cfg_.force_algo = Algo::IPC_DYN;
+  else TORCH_CHECK(false, "set_algo: expected auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|host, got ", a);
 }
 
 void ProcessGroupMI355X::set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max) {

@@ -571,6 +571,7 @@ class ProcessGroupMI355X : public c10d::Backend {
     std::string ref;  // reference engine: rccl, or host where RCCL is unavailable
     double rccl_us, ipc_us;
     double push_us;   // push all-reduce (0 = not raced)
+    double dyn_us = 0;  // dynamic 2-shot all-reduce (0 = not raced)
     double wide_us;   // RCCL on the wide child communicator (0 = not raced)
     double ipc_wide_us;  // pull all-reduce with ipc_wide_grid workgroups (0 = not raced)
     double staged_us;    // IPC with zero copy off (0 = not raced)
@@ -592,7 +593,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // online autotuner (gpu_ops.cpp)
   struct TuneEntry {
     Algo ref = Algo::RCCL;
-    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0, ipc_wide_us = 0, staged_us = 0;
+    double rccl_us = 0, ipc_us = 0, push_us = 0, wide_us = 0, ipc_wide_us = 0, staged_us = 0, dyn_us = 0;
     bool valid = false;
     Algo algo = Algo::AUTO;
     int iters = 0;

@@ -160,6 +160,7 @@ PYBIND11_MODULE(_C, m) {
                d["ref_us"] = r.rccl_us;
                d["ipc_us"] = r.ipc_us;
                d["push_us"] = r.push_us;
+               d["dyn_us"] = r.dyn_us;
                d["wide_us"] = r.wide_us;
                d["ipc_wide_us"] = r.ipc_wide_us;
                d["staged_us"] = r.staged_us;

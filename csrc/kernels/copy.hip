@@ -336,7 +336,7 @@ hipError_t multi_copy(const CopyDesc* descs, int n, hipStream_t stream, int max_
 }
 
 // block-pairwise flags, the per-block call counters, the LL control words and LL slots
-size_t ipc_signal_bytes() { return kZxOffset + kZxBytes; }
+size_t ipc_signal_bytes() { return kDynOffset + kDynBytes; }
 
 size_t ipc_staging_bytes(const IpcCall& c, int world) {
   if (c.gate) {  // either protocol may run: the larger need

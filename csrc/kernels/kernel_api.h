@@ -221,6 +221,33 @@ constexpr size_t kZxEpochOffset = kZxOffset + kMaxRanks * kZxSrcBytes;
 constexpr size_t kZxResolvedOffset = kZxOffset + 1024;
 constexpr size_t kZxBytes = 1024 + kGateSlots * sizeof(GateSlot);
 
+// Dynamic zero-copy 2-shot all-reduce (IpcCall::dyn): instead of a fixed tile range per
+// workgroup and a block-pairwise barrier between the phases, the workgroups of a rank claim
+// work items from a counter in its signal area -- first "reduce my tiles of chunk i" (then
+// publish chunk i's ready word), then "copy peer q's reduced tiles of chunk c" (after q's
+// ready word for c) -- so fast workgroups take more items and a chunk's second phase starts
+// as soon as its owner reduced it. The call ends when every rank's last workgroup has seen
+// every peer's "done" word (no peer reads this rank's tensor any more).
+// Own signal area after the exchange area: control words, per-source done words, then one
+// ready word per chunk. Words hold a per-rank dyn-call epoch (never 0), compared for equality.
+constexpr size_t kDynOffset = kZxOffset + kZxBytes;
+constexpr int kDynEpochWord = 0;   // u32 at kDynOffset: epoch of this rank's last finished dyn call
+constexpr int kDynClaimWord = 1;   // work-item counter of the running call (reset by its last block)
+constexpr int kDynExitWord = 2;    // blocks of the running call that finished (reset by the last one)
+constexpr size_t kDynDoneOffset = kDynOffset + 64;    // u32 per source rank: its last block's epoch
+constexpr size_t kDynReadyOffset = kDynOffset + 128;  // u32 per chunk: the epoch its owner reduced it in
+constexpr uint32_t kDynMaxChunks = 16384;
+constexpr uint32_t kDynMinRows = 4;  // rows (W tiles each) per chunk, at least
+constexpr size_t kDynBytes = 128 + (size_t)kDynMaxChunks * 4;
+// rows per chunk of a dyn call: about 4 chunks per workgroup, at least kDynMinRows rows, at
+// most kDynMaxChunks chunks (a function of the call's shape only: identical on every rank)
+__host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid) {
+  size_t k = nrows / (4 * (size_t)(grid ? grid : 1));
+  if (k < kDynMinRows) k = kDynMinRows;
+  const size_t lo = (nrows + kDynMaxChunks - 1) / kDynMaxChunks;
+  return (uint32_t)(k < lo ? lo : k);
+}
+
 template <template <class> class P>
 struct IpcCallT {
   IpcColl coll;
@@ -250,6 +277,7 @@ struct IpcCallT {
   uint64_t zx_off;
   P<char> zx_self;
   P<const ZcTable> ztab;
+  int dyn;  // 1: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol (see kDynOffset); staged runs ignore it
 };
 using IpcCall = IpcCallT<RawPtr>;
 

@@ -332,6 +332,112 @@ struct PeerTileMap {
   }
 };
 
+// ---- dynamic zero-copy 2-shot all-reduce (IpcCall::dyn, layout at kern::kDynOffset) --------
+__device__ __forceinline__ uint32_t* dyn_words(const DView& v, int rank, size_t off) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>((uint32_t*)v.flags[rank]) + off);
+}
+
+// Thread 0: bounded poll until *w == want (system scope); false on timeout (error word set) or
+// when the group was aborted / another block timed out, so the grid always drains.
+__device__ __forceinline__ bool dyn_wait(const DView& v, const uint32_t* w, uint32_t want, uint32_t code) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (uint32_t it = 1;; ++it) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == want) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
+      __hip_atomic_store(static_cast<uint32_t*>(v.err), code | (uint32_t)v.rank, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    if ((it & 255u) == 0 &&
+        __hip_atomic_load(static_cast<uint32_t*>(v.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Rows of W tiles (tile q + W*r belongs to rank q), K rows per chunk, nc chunks. Work items,
+// claimed in order from this rank's counter: [0, nc) reduce my tiles of chunk i from every
+// rank's tensor, in place (read-once loads), then publish ready[i] = dep; [nc, W*nc) copy
+// peer q's tiles of chunk c into my tensor once q's ready[c] == dep (peers rotated per chunk,
+// so the items in flight spread over every xGMI link). Every phase-1 item of a rank is claimed
+// before any of its phase-2 items and a phase-1 item waits for nothing, so every ready word a
+// phase-2 item waits for is eventually published: no cycle. Overwrites are safe: the peer
+// positions I write in phase 2 (tile q + W*r of MY tensor) were read by q in its phase 1 of
+// chunk c, which q finished before publishing ready[c]; my own tiles are written in phase 1
+// only, and peers read them after my ready word.
+template <DType DT, RedOp OP, int W>
+__device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds) {
+  constexpr int D = DepthFor<W>::value;
+  const int me = v.rank;
+  const size_t nrows = c.bytes / kTile / W;
+  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x);
+  const uint32_t nc = (uint32_t)((nrows + K - 1) / K), total = nc * W;
+  uint32_t* const ctl = dyn_words(v, me, kern::kDynOffset);
+  uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
+  __shared__ uint32_t s_dep, s_item, s_ok;
+  if (threadIdx.x == 0) {  // this call's epoch (the previous dyn call's last block stored its own)
+    uint32_t e = __hip_atomic_load(ctl + kern::kDynEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    s_dep = e ? e : 1u;
+  }
+  __syncthreads();
+  const uint32_t dep = s_dep;
+  bool ok = true;
+  for (;;) {
+    if (threadIdx.x == 0)
+      s_item = __hip_atomic_fetch_add(ctl + kern::kDynClaimWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t it = s_item;
+    __syncthreads();  // (s_item is rewritten by the next claim)
+    if (it >= total) break;
+    if (it < nc) {
+      const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
+      const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
+      ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
+      drain_vm();  // every wave's stores and loads (a peer overwrites what I read once it sees ready)
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
+        drain_vm();
+        __hip_atomic_store(ready + it, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    } else {
+      const uint32_t j = it - nc, cc = j / (W - 1), k = j - cc * (W - 1);
+      const int q = (me + 1 + (int)((k + cc) % (W - 1))) % W;
+      if (threadIdx.x == 0) {
+        s_ok = ok && dyn_wait(v, dyn_words(v, q, kern::kDynReadyOffset) + cc, dep, 0x800u) ? 1u : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
+        drain_vm();
+      }
+      __syncthreads();
+      ok = s_ok != 0;
+      __syncthreads();
+      if (ok) {
+        const size_t r0 = (size_t)cc * K, r1 = r0 + K < nrows ? r0 + K : nrows;
+        const OneSrcMap m{v.buf[q], v.buf[me], c.bytes, (size_t)q + W * r0, W, W * r1};
+        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      }
+    }
+  }
+  // departure: once every block of mine is done, tell the peers; the last block waits until every
+  // peer's blocks are done too (nobody reads my tensor any more), then resets the counters
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(ctl + kern::kDynExitWord, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      for (int q = 0; q < W; ++q)
+        if (q != me)
+          __hip_atomic_store(dyn_words(v, q, kern::kDynDoneOffset) + me, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t* const done = dyn_words(v, me, kern::kDynDoneOffset);
+      for (int q = 0; q < W; ++q)
+        if (q != me && ok) ok = dyn_wait(v, done + q, dep, 0x900u);
+      __hip_atomic_store(ctl + kern::kDynClaimWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + kern::kDynExitWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + kern::kDynEpochWord, dep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
 // The arrival barrier is a data barrier here -- it hands over each rank's input,
 // written by the kernels before this one -- and a departure barrier ends the call:
@@ -348,6 +454,11 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   block_barrier(v, ep);
   tr.mark(2);
   tr.mark(4);
+  if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
+    ipc_allreduce_dyn<DT, OP, W>(v, c, lds);
+    tr.mark(5);
+    return;
+  }
   if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
     {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};

@@ -367,6 +367,8 @@ def run(rank: int, world: int, dev, deadline_s: float = 45.0, max_bytes: int = 6
             P.check("zc/broadcast", gb, zc_broadcast, expect_engine="ipc_2shot_zc")
             set_engine("ipc_push")
             P.check("zc/all_reduce_push", gb, zc_all_reduce, expect_engine="ipc_push_zc")
+            set_engine("ipc_dyn")
+            P.check("zc/all_reduce_dyn", gb, zc_all_reduce, expect_engine="ipc_2shot_dyn_zc")
     set_engine("auto")
     out = P.result()
     out["info"] = info

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Static vs dynamic zero-copy 2-shot all_reduce, ranks sharing one GPU.
+
+PDCC_ALGO=ipc runs the static protocol (a fixed tile range per workgroup, block-pairwise
+barrier between the phases); PDCC_ALGO=ipc_dyn the dynamic one (work items claimed per
+workgroup from a counter, per-chunk ready words; kern::kDynOffset). Median wall time of
+`--iters` synchronous all_reduces (max over ranks) per size, correctness checked, and the
+busbw-style HBM rate of the whole call (both ranks' traffic on the one GPU).
+
+    python scripts/dyn_bench.py [--world 2] [--mib 16,64,256] [--iters 20]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def work(rank, size, mibs, iters):
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    b = be.native_backend(None, "cuda")
+    out = {}
+    for mib in mibs:
+        n = (mib << 20) // 4
+        x = torch.empty(n, device=dev)
+        for _ in range(3):
+            x.fill_(float(rank + 1))
+            dist.all_reduce(x)
+        torch.cuda.synchronize()
+        lat, ok = [], True
+        for i in range(iters):
+            x.fill_(float(rank + 1 + i % 5))
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            dist.all_reduce(x)
+            torch.cuda.synchronize()
+            engine = b.last_algo()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            lat.append(t.item())
+            ok = ok and bool(torch.all(x == float(sum(r + 1 + i % 5 for r in range(size)))))
+        us = statistics.median(lat) * 1e6
+        out[mib] = {"us": round(us, 1), "engine": engine, "correct": ok}
+        del x
+        torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--mib", default="16,64,256")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--algos", default="ipc,ipc_dyn")
+    a = ap.parse_args()
+    from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
+
+    mibs = [int(m) for m in a.mib.split(",")]
+    res = {}
+    for algo in a.algos.split(","):
+        env = {"PDCC_ALGO": algo, "PDCC_AUTOTUNE": "0"}
+        r = launch(work, a.world, args=(mibs, a.iters), bind_device=True, timeout_s=120, env=env, join_timeout_s=500)
+        res[algo] = r[0]
+        for mib, v in r[0].items():
+            W, S = a.world, mib << 20
+            # HBM bytes of one zero-copy 2-shot call, all ranks on one GPU (scripts/ipc_phase_trace.py)
+            rate = (W * S * (1 + (W - 1) / W) + W * S) / (v["us"] * 1e-6) / 1e12
+            print(json.dumps({"world_on_one_gpu": W, "algo": algo, "mib": mib, **v, "hbm_TBps": round(rate, 2)}),
+                  flush=True)
+    algos = a.algos.split(",")
+    if len(algos) == 2:
+        sp = {m: round(res[algos[0]][m]["us"] / res[algos[1]][m]["us"], 3) for m in mibs}
+        print(json.dumps({"world_on_one_gpu": a.world, f"speedup_{algos[1]}_over_{algos[0]}": sp}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1444,7 +1444,8 @@ def zc_burst_probe(rank, size, device="cuda", calls=64, n=(4 << 20) // 4):
 
 # elements per case: every size ragged (not a multiple of a 4 KiB tile or of W tiles)
 _NUMERICS_SIZES = {"ll": (1, 777, 16381), "oneshot": (40_009, 100_003), "twoshot": (300_007, 1_000_003),
-                   "zc": (700_001, 2_000_003), "push": (700_001, 2_000_003), "staged_algo": (700_001, 2_000_003)}
+                   "zc": (700_001, 2_000_003), "push": (700_001, 2_000_003), "staged_algo": (700_001, 2_000_003),
+                   "dyn": (700_001, 2_000_003, 9_000_011)}
 
 
 def random_numerics(rank, size, device="cuda", mode="ll"):
@@ -1776,3 +1777,38 @@ def phase_trace_probe(rank, size, device="cuda", calls=6, mib=8):
         out["slowest_exit_after_block0_us"] = (max(ex) - r[7]) / 100.0 if ex else None
         out["phase1_before_exit"] = all(a <= e for a, e in zip(r[HDR:HDR + NB], r[HDR + NB:HDR + 2 * NB]) if a)
     return out
+
+
+def dyn_stress(rank, size, device="cuda", calls=60):
+    """The dynamic zero-copy all-reduce (PDCC_ALGO=ipc_dyn) over many calls: sizes from a few
+    chunks to thousands, synchronous and async (capped grid: another chunk size), interleaved
+    with LL all_reduces and a barrier; integer-valued data so every sum is exact."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    sizes = [(1 << 20) // 4, (8 << 20) // 4 + 3, (64 << 20) // 4, (3 << 20) // 4 + 1024]
+    bufs = [torch.empty(n, device=d) for n in sizes]
+    small = torch.empty(1000, device=d)
+    ok, engines = True, set()
+    for i in range(calls):
+        x = bufs[i % len(bufs)]
+        x.fill_(float(rank + 1 + i % 7))
+        if i % 3 == 2:
+            dist.all_reduce(x, async_op=True).wait()
+        else:
+            dist.all_reduce(x)
+        engines.add(b.last_algo())
+        want = float(sum(r + 1 + i % 7 for r in range(size)))
+        ok = ok and bool(torch.all(x == want))
+        if i % 5 == 4:
+            small.fill_(1.0)
+            dist.all_reduce(small)
+            ok = ok and bool(torch.all(small == size))
+        if i % 11 == 10:
+            dist.barrier()
+    torch.cuda.synchronize()
+    return {"ok": ok, "engines": sorted(engines), "desc": b.describe()}

@@ -180,7 +180,7 @@ def test_autotuner_shared_gpu():
     assert los == [64 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20], res[0]["table"]
     for e in res[0]["table"]:
         assert e["coll"] == "allreduce" and e["ipc_valid"], e
-        assert e["algo"] in ("ipc", "ipc_push", "ipc_staged", "host") and e["ref"] == "host"
+        assert e["algo"] in ("ipc", "ipc_push", "ipc_staged", "ipc_dyn", "host") and e["ref"] == "host"
         assert e["dtype"] in ("Float", "BFloat16") and e["op"] == "SUM", e
         assert e["iters"] >= 3
 
@@ -199,7 +199,7 @@ def test_autotuner_every_collective_shared_gpu():
                  ("allreduce", "Int", "BAND"), ("allreduce", "Int", "BOR")]:
         assert want in rows, (want, sorted(rows))
     for e in res[0]["table"]:
-        assert e["ipc_valid"] and e["algo"] in ("ipc", "ipc_push", "ipc_staged", "host"), e
+        assert e["ipc_valid"] and e["algo"] in ("ipc", "ipc_push", "ipc_staged", "ipc_dyn", "host"), e
 
 
 def test_autotune_ipc_timeout_is_contained():
@@ -464,6 +464,8 @@ _NUMERICS_ENV = {
     "push": ({"PDCC_ALGO": "ipc_push", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_push"),
     # the autotuner's staged candidate at zero-copy sizes (IPC with zero copy off for the call)
     "staged_algo": ({"PDCC_ALGO": "ipc_staged", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_2shot"),
+    # the dynamic zero-copy 2-shot (work items claimed per workgroup, per-chunk ready words)
+    "dyn": ({"PDCC_ALGO": "ipc_dyn", "PDCC_IPC_1SHOT_MAX": "64K"}, "ipc_2shot_dyn"),
 }
 
 
@@ -480,6 +482,16 @@ def test_random_numerics_every_protocol(mode, world):
             assert engines == {"ipc_2shot"}, engines
         else:
             assert all(e.startswith(want) for e in engines), engines
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dynamic_allreduce_many_calls(world):
+    # the dynamic protocol's per-rank epoch, claim and exit counters over 60 calls of four sizes,
+    # sync and async (capped grid), between LL all_reduces and barriers: every sum exact
+    env = {"PDCC_ALGO": "ipc_dyn", "PDCC_IPC_1SHOT_MAX": "64K"}
+    for r in _gpu_launch(W.dyn_stress, world, env=env, timeout_s=120):
+        assert r["ok"], r
+        assert "ipc_2shot_dyn_zc" in r["engines"], r["engines"]
 
 
 def test_autotune_file_persists_decisions(tmp_path):
