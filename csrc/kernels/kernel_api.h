@@ -237,12 +237,12 @@ constexpr int kDynExitWord = 2;    // blocks of the running call that finished (
 constexpr size_t kDynDoneOffset = kDynOffset + 64;    // u32 per source rank: its last block's epoch
 constexpr size_t kDynReadyOffset = kDynOffset + 128;  // u32 per chunk: the epoch its owner reduced it in
 constexpr uint32_t kDynMaxChunks = 16384;
-constexpr uint32_t kDynMinRows = 4;  // rows (W tiles each) per chunk, at least
+constexpr uint32_t kDynMinRows = 8;  // rows (W tiles each) per chunk, at least
 constexpr size_t kDynBytes = 128 + (size_t)kDynMaxChunks * 4;
-// rows per chunk of a dyn call: about 4 chunks per workgroup, at least kDynMinRows rows, at
+// rows per chunk of a dyn call: about 3 chunks per workgroup, at least kDynMinRows rows, at
 // most kDynMaxChunks chunks (a function of the call's shape only: identical on every rank)
 __host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid) {
-  size_t k = nrows / (4 * (size_t)(grid ? grid : 1));
+  size_t k = nrows / (3 * (size_t)(grid ? grid : 1));
   if (k < kDynMinRows) k = kDynMinRows;
   const size_t lo = (nrows + kDynMaxChunks - 1) / kDynMaxChunks;
   return (uint32_t)(k < lo ? lo : k);

@@ -120,13 +120,14 @@ def main():
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="zc,staged")
+    ap.add_argument("--algo", default="ipc", help="PDCC_ALGO of the traced calls (ipc, ipc_dyn, ...)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     S = a.mib << 20
     W = a.world
     for mode in a.modes.split(","):
-        env = {"PDCC_ALGO": "ipc", "PDCC_IPC_TRACE": "64", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
+        env = {"PDCC_ALGO": a.algo, "PDCC_IPC_TRACE": "64", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
                "PDCC_AUTOTUNE": "0"}
         res = launch(work, W, args=(a.mib, a.iters), bind_device=True, timeout_s=120, env=env, join_timeout_s=400)
         # HBM bytes per call, all ranks together (one GPU): reads / writes
@@ -135,7 +136,7 @@ def main():
         else:
             rd, wr = W * S * (2 + (W - 1) / W), W * S * (1 + 1 + 1 / W)
         for r in res:
-            r.update(mode=mode, world_on_one_gpu=W, bytes=S, hbm_read_bytes=int(rd), hbm_write_bytes=int(wr))
+            r.update(mode=mode, algo=a.algo, world_on_one_gpu=W, bytes=S, hbm_read_bytes=int(rd), hbm_write_bytes=int(wr))
             kt = r["phases_us"]["kernel_total"]
             if kt:
                 r["hbm_TBps_kernel"] = round((rd + wr) / (kt * 1e-6) / 1e12, 2)
