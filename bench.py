@@ -475,7 +475,7 @@ def algo_ab(world, rank, dev, native, x, out):
 
     big = (1 << 30) if not SMALL else (64 << 20)
     rccl_ok = "rccl_ok=1" in native.describe()
-    algos = ("rccl", "ipc", "ipc_push") if rccl_ok else ("ipc", "ipc_push")
+    algos = ("rccl", "ipc", "ipc_push", "ipc_dyn") if rccl_ok else ("ipc", "ipc_push", "ipc_dyn")
     if not rccl_ok:
         out["rccl_rows"] = "dropped: ranks share a GPU, RCCL unavailable"
     for algo in algos:
@@ -483,7 +483,7 @@ def algo_ab(world, rank, dev, native, x, out):
             gb.set_algo(algo)
             progress(f"algo A/B: {algo}")
             for nbytes in (4, 64 << 10, 1 << 20, 16 << 20, 256 << 20, big):
-                if nbytes == 256 << 20 and SMALL or (algo == "ipc_push" and nbytes < (1 << 20)):
+                if nbytes == 256 << 20 and SMALL or (algo in ("ipc_push", "ipc_dyn") and nbytes < (1 << 20)):
                     continue
                 t = x[: nbytes // 4]
                 lat = _time_op(lambda: dist.all_reduce(t, group=g), 10 if nbytes >= (16 << 20) else 50)
@@ -498,7 +498,7 @@ def algo_ab(world, rank, dev, native, x, out):
             # the other collectives at 1 MiB and the big size (S = total bytes, nccl-tests factors)
             from pytorch_distributed_collective_communication_amd.utils import busbw as bb
 
-            for nbytes in ((1 << 20, big) if algo != "ipc_push" else ()):  # push: all_reduce only
+            for nbytes in ((1 << 20, big) if algo not in ("ipc_push", "ipc_dyn") else ()):  # push/dyn: all_reduce only
                 per = nbytes // 4 // world
                 src = x[:per]
                 full = torch.empty(per * world, device=dev)
