@@ -40,7 +40,7 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
       bytes > cfg_.ipc_1shot_max)
     v.push_back(Algo::IPC_PUSH);
   // the dynamic 2-shot all-reduce (zero-copy sizes): work items claimed per workgroup
-  if (c == Coll::ALLREDUCE && cfg_.ipc_dyn && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
+  if (c == Coll::ALLREDUCE && cfg_.ipc_dyn > 0 && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
       bytes > cfg_.ipc_1shot_max)
     v.push_back(Algo::IPC_DYN);
   return v;

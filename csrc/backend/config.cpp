@@ -84,7 +84,7 @@ Config Config::from_env() {
   c.ipc_selftest_ms = env_int("PDCC_IPC_SELFTEST_MS", c.ipc_selftest_ms);
   c.ipc_zc = env_bool("PDCC_IPC_ZC", c.ipc_zc);
   c.ipc_push = env_bool("PDCC_IPC_PUSH", c.ipc_push);
-  c.ipc_dyn = env_bool("PDCC_IPC_DYN", c.ipc_dyn);
+  c.ipc_dyn = std::min(64, std::max(0, env_int("PDCC_IPC_DYN", c.ipc_dyn)));
   c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
   c.ipc_ll_max = env_size("PDCC_IPC_LL_MAX", c.ipc_ll_max);
   c.ipc_zc_cache = std::max<size_t>(1, env_size("PDCC_IPC_ZC_CACHE", c.ipc_zc_cache));

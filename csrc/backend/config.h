@@ -44,7 +44,9 @@ struct Config {
   // The autotuner also races the push all-reduce (owners receive their tiles by remote writes,
   // reduce locally and write the result into every rank's tensor) for zero-copy sizes.
   bool ipc_push = true;                    // PDCC_IPC_PUSH
-  bool ipc_dyn = true;                     // PDCC_IPC_DYN: race the dynamic 2-shot all-reduce (IPC_DYN)
+  // PDCC_IPC_DYN: chunks per workgroup of the dynamic 2-shot all-reduce (IPC_DYN; fewer = less
+  // per-item overhead, more = finer load balance); 0: the autotuner does not race it (0..64)
+  int ipc_dyn = 3;
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
   // All-reduces up to this size (<= 256 KiB, kern::kLLMaxBytes) use the LL protocol: every
   // rank pushes flag-tagged 8-byte words into its peers' signal areas and polls its own --

@@ -332,7 +332,8 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
                     : (one_shot ? kern::IpcColl::ALLREDUCE_1SHOT : kern::IpcColl::ALLREDUCE_2SHOT);
     if (a == Algo::IPC_PUSH && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.coll = kern::IpcColl::ALLREDUCE_PUSH;
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
-    if (a == Algo::IPC_DYN && c.coll == kern::IpcColl::ALLREDUCE_2SHOT) c.dyn = 1;  // (zero-copy runs only)
+    if (a == Algo::IPC_DYN && c.coll == kern::IpcColl::ALLREDUCE_2SHOT)  // (zero-copy runs only)
+      c.dyn = std::max(1, cfg_.ipc_dyn);  // chunks per workgroup
     // small (all-)reduce: flag-tagged pushes, no staging copy, no barrier
     if (ds.ll_ok && bytes_in_ll_range(w.nbytes()))
       c.coll = rooted ? kern::IpcColl::REDUCE_LL : kern::IpcColl::ALLREDUCE_LL;

@@ -124,25 +124,28 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
 
   // The IPC workgroup caps must be the same on every rank (the block-pairwise protocol pairs block b of
   // every rank): a rank started with different PDCC_IPC_GRID / _WIDE_GRID / _ASYNC_GRID settings is
-  // brought to the group's minimum instead of hanging its peers' barriers.
+  // brought to the group's minimum instead of hanging its peers' barriers. PDCC_IPC_DYN likewise: it
+  // sets the dynamic all-reduce's chunk size (every rank must number the chunks alike) and whether the
+  // autotuner races it (every rank must race the same candidates).
   {
-    const int32_t mine3[3] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid};
+    const int32_t mine3[4] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid, cfg_.ipc_dyn};
     const auto gv = store_allgather(store_, "pdcc/dev_grids", rank_, size_,
                                     std::vector<uint8_t>(reinterpret_cast<const uint8_t*>(mine3),
                                                          reinterpret_cast<const uint8_t*>(mine3) + sizeof(mine3)));
-    int32_t lo[3] = {mine3[0], mine3[1], mine3[2]};
+    int32_t lo[4] = {mine3[0], mine3[1], mine3[2], mine3[3]};
     for (const auto& v : gv) {
       if (v.size() != sizeof(mine3)) continue;
-      int32_t t[3];
+      int32_t t[4];
       std::memcpy(t, v.data(), sizeof(t));
-      for (int k = 0; k < 3; ++k) lo[k] = std::min(lo[k], t[k]);
+      for (int k = 0; k < 4; ++k) lo[k] = std::min(lo[k], t[k]);
     }
-    if (lo[0] != mine3[0] || lo[1] != mine3[1] || lo[2] != mine3[2])
-      fprintf(stderr, "[pdcc r%d] IPC grid caps differ between ranks: using the group minimum %d/%d/%d\n", rank_,
-              lo[0], lo[1], lo[2]);
+    if (lo[0] != mine3[0] || lo[1] != mine3[1] || lo[2] != mine3[2] || lo[3] != mine3[3])
+      fprintf(stderr, "[pdcc r%d] IPC grid caps / PDCC_IPC_DYN differ between ranks: using the group minimum "
+              "%d/%d/%d/%d\n", rank_, lo[0], lo[1], lo[2], lo[3]);
     cfg_.ipc_grid = std::max(1, lo[0]);
     cfg_.ipc_wide_grid = lo[1];
     cfg_.ipc_async_grid = lo[2];
+    cfg_.ipc_dyn = lo[3];
   }
   ds.recs = recs;
   ds.shared_device = shared;

@@ -239,10 +239,11 @@ constexpr size_t kDynReadyOffset = kDynOffset + 128;  // u32 per chunk: the epoc
 constexpr uint32_t kDynMaxChunks = 16384;
 constexpr uint32_t kDynMinRows = 8;  // rows (W tiles each) per chunk, at least
 constexpr size_t kDynBytes = 128 + (size_t)kDynMaxChunks * 4;
-// rows per chunk of a dyn call: about 3 chunks per workgroup, at least kDynMinRows rows, at
-// most kDynMaxChunks chunks (a function of the call's shape only: identical on every rank)
-__host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid) {
-  size_t k = nrows / (3 * (size_t)(grid ? grid : 1));
+// rows per chunk of a dyn call: about `per` chunks per workgroup (IpcCall::dyn, PDCC_IPC_DYN), at least
+// kDynMinRows rows, at most kDynMaxChunks chunks (a function of the call's shape and a group-wide
+// setting only: identical on every rank)
+__host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid, uint32_t per) {
+  size_t k = nrows / ((size_t)(per ? per : 1) * (size_t)(grid ? grid : 1));
   if (k < kDynMinRows) k = kDynMinRows;
   const size_t lo = (nrows + kDynMaxChunks - 1) / kDynMaxChunks;
   return (uint32_t)(k < lo ? lo : k);
@@ -277,7 +278,8 @@ struct IpcCallT {
   uint64_t zx_off;
   P<char> zx_self;
   P<const ZcTable> ztab;
-  int dyn;  // 1: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol (see kDynOffset); staged runs ignore it
+  int dyn;  // > 0: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol with about `dyn` chunks per
+            // workgroup (see kDynOffset); staged runs ignore it
 };
 using IpcCall = IpcCallT<RawPtr>;
 

@@ -370,7 +370,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
   constexpr int D = DepthFor<W>::value;
   const int me = v.rank;
   const size_t nrows = c.bytes / kTile / W;
-  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x);
+  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn);
   const uint32_t nc = (uint32_t)((nrows + K - 1) / K), total = nc * W;
   uint32_t* const ctl = dyn_words(v, me, kern::kDynOffset);
   uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);

@@ -21,7 +21,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
 | PDCC_IPC_ASYNC_GRID | 64 | workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; must agree across ranks like async_op itself (0: no cap) |
 | PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
-| PDCC_IPC_DYN | 1 | race the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier) for zero-copy all_reduce keys |
+| PDCC_IPC_DYN | 3 | chunks per workgroup of the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier), which the autotuner races for zero-copy all_reduce keys; 0: not raced; agreed group-wide (minimum) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
@@ -87,7 +87,7 @@ class Config:
     ipc_max_staging: int = 1 << 30
     ipc_zc: bool = True
     ipc_push: bool = True
-    ipc_dyn: bool = True
+    ipc_dyn: int = 3
     ipc_zc_min: int = 1 << 20
     ipc_ll_max: int = 256 << 10
     ipc_zc_cache: int = 16

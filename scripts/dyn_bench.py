@@ -60,14 +60,17 @@ def main():
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--mib", default="16,64,256")
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--algos", default="ipc,ipc_dyn")
+    ap.add_argument("--algos", default="ipc,ipc_dyn",
+                    help="PDCC_ALGO values; ipc_dyn@N also sets PDCC_IPC_DYN=N (chunks per workgroup)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     mibs = [int(m) for m in a.mib.split(",")]
     res = {}
     for algo in a.algos.split(","):
-        env = {"PDCC_ALGO": algo, "PDCC_AUTOTUNE": "0"}
+        env = {"PDCC_ALGO": algo.split("@")[0], "PDCC_AUTOTUNE": "0"}
+        if "@" in algo:
+            env["PDCC_IPC_DYN"] = algo.split("@")[1]
         r = launch(work, a.world, args=(mibs, a.iters), bind_device=True, timeout_s=120, env=env, join_timeout_s=500)
         res[algo] = r[0]
         for mib, v in r[0].items():
