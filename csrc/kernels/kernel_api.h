@@ -231,14 +231,15 @@ constexpr size_t kZxBytes = 1024 + kGateSlots * sizeof(GateSlot);
 // Own signal area after the exchange area: control words, per-source done words, then one
 // ready word per chunk. Words hold a per-rank dyn-call epoch (never 0), compared for equality.
 constexpr size_t kDynOffset = kZxOffset + kZxBytes;
-constexpr int kDynEpochWord = 0;   // u32 at kDynOffset: epoch of this rank's last finished dyn call
-constexpr int kDynClaimWord = 1;   // work-item counter of the running call (reset by its last block)
-constexpr int kDynExitWord = 2;    // blocks of the running call that finished (reset by the last one)
-constexpr size_t kDynDoneOffset = kDynOffset + 64;    // u32 per source rank: its last block's epoch
-constexpr size_t kDynReadyOffset = kDynOffset + 128;  // u32 per chunk: the epoch its owner reduced it in
+// (u32 word indices from kDynOffset; the two counters every block hits sit 128 B apart)
+constexpr int kDynEpochWord = 0;   // epoch of this rank's last finished dyn call
+constexpr int kDynClaimWord = 32;  // work-item counter of the running call (reset by its last block)
+constexpr int kDynExitWord = 64;   // blocks of the running call that finished (reset by the last one)
+constexpr size_t kDynDoneOffset = kDynOffset + 384;   // u32 per source rank: its last block's epoch
+constexpr size_t kDynReadyOffset = kDynOffset + 512;  // u32 per chunk: the epoch its owner reduced it in
 constexpr uint32_t kDynMaxChunks = 16384;
 constexpr uint32_t kDynMinRows = 8;  // rows (W tiles each) per chunk, at least
-constexpr size_t kDynBytes = 128 + (size_t)kDynMaxChunks * 4;
+constexpr size_t kDynBytes = 512 + (size_t)kDynMaxChunks * 4;
 // rows per chunk of a dyn call: about `per` chunks per workgroup (IpcCall::dyn, PDCC_IPC_DYN), at least
 // kDynMinRows rows, at most kDynMaxChunks chunks (a function of the call's shape and a group-wide
 // setting only: identical on every rank)

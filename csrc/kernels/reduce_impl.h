@@ -382,11 +382,12 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
   __syncthreads();
   const uint32_t dep = s_dep;
   bool ok = true;
-  // thread 0 claims one item ahead: the atomic's round trip overlaps the current item (claims
-  // are monotonic, so a held phase-1 item is never behind a phase-2 wait of the same block)
-  uint32_t next = 0;
-  if (threadIdx.x == 0)
-    next = __hip_atomic_fetch_add(ctl + kern::kDynClaimWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // Block b's first item is item b (no counter traffic at launch: every block hitting one uncached
+  // word at once serialises at the memory controller -- a fixed ~17 us at any size on one MI355X);
+  // later items are G + the counter. Thread 0 claims one item ahead, so the atomic's round trip
+  // overlaps the current item. Claims are monotonic (b < G <= G + k), so a held phase-1 item is
+  // never behind a phase-2 wait of the same block.
+  uint32_t next = blockIdx.x;
   for (;;) {
     if (threadIdx.x == 0) s_item = next;
     __syncthreads();
@@ -394,7 +395,8 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
     __syncthreads();  // (s_item is rewritten by the next claim)
     if (it >= total) break;
     if (threadIdx.x == 0)
-      next = __hip_atomic_fetch_add(ctl + kern::kDynClaimWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      next = gridDim.x +
+             __hip_atomic_fetch_add(ctl + kern::kDynClaimWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};

@@ -61,7 +61,10 @@ def work(rank, size, mib, iters):
         return round(statistics.median(v), 1) if v else None
 
     phases = {"entry_to_arrival": ph(1, 2), "arrival_to_data_barrier": ph(2, 4), "stage_or_gate": ph(2, 3),
-              "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7)}
+              "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7),
+              # block 0's device-side buffer exchange of a gated zero-copy launch (words 8-11)
+              "zx_records_in": ph(1, 8), "zx_lookup": ph(8, 9), "zx_votes_in": ph(9, 10), "zx_published": ph(10, 11),
+              "zx_to_arrival": ph(11, 2)}
     out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
            "phases_us": phases, "records": len(recs), "blocks_us": block_spread(recs)}
     # K1 at the same total workgroup budget: rank 0 alone, the others wait
