@@ -115,6 +115,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
+  if (const char* tf = std::getenv("PDCC_TEST_IPC_FLAGS")) test_flags_ = std::atoi(tf);
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   closing_limit_ = std::max<size_t>(2, (size_t)kern::kZcTab > zc_cache_ ? (size_t)kern::kZcTab - zc_cache_ : 0);
   if (world < 2 || world > kern::kMaxRanks)
@@ -325,6 +326,7 @@ kern::IpcView IpcComm::view(const std::vector<char*>& bufs) const {
 
 void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_t stream) {
   ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
+  call.test_flags = test_flags_;
   if (shared_device_) {
     // all ranks' grids must be co-resident on ONE device (test setups): stay well
     // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels

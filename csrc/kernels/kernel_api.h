@@ -281,6 +281,8 @@ struct IpcCallT {
   P<const ZcTable> ztab;
   int dyn;  // > 0: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol with about `dyn` chunks per
             // workgroup (see kDynOffset); staged runs ignore it
+  int test_flags;  // PDCC_TEST_IPC_FLAGS, measurements only: bit 0 = the zero-copy reductions' arrival
+                   // barrier without its release / acquire (what the data hand-over costs)
 };
 using IpcCall = IpcCallT<RawPtr>;
 

@@ -459,7 +459,8 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
   const size_t nt = c.bytes / kTile;
-  block_barrier(v, ep);
+  if (c.test_flags & 1) block_barrier<false>(v, ep);  // (measurement hook, see IpcCall::test_flags)
+  else block_barrier(v, ep);
   tr.mark(2);
   tr.mark(4);
   if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
