@@ -207,8 +207,8 @@ PYBIND11_MODULE(_C, m) {
       .def("abort_group", &pdcc::ProcessGroupMI355X::abort_group, py::call_guard<py::gil_scoped_release>())
       .def("ipc_trace", &pdcc::ProcessGroupMI355X::ipc_trace,
            "PDCC_IPC_TRACE records: [seq, t_entry, t_seq, t_staged, t_barrier0, t_phase1, t_barrier1, t_exit] "
-           "in 100 MHz device ticks, block 0 of each IPC kernel (words 8-11: zero-copy exchange), then per block "
-           "b < 256: [12 + b] phase 1 done, [268 + b] exit")
+           "in 100 MHz device ticks, block 0 of each IPC kernel (words 8-11: zero-copy exchange, 12-15: call number "
+           "and zero-copy arrival barrier), then per block b < 256: [16 + b] phase 1 done, [272 + b] exit")
       .def("eager_init", &pdcc::ProcessGroupMI355X::eager_init, py::arg("device"),
            py::call_guard<py::gil_scoped_release>())
       // torch calls this on non-member ranks of a new group when the default group is bound

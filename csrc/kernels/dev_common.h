@@ -492,13 +492,14 @@ __device__ __forceinline__ bool reached(uint32_t have, uint32_t want) {
 // staging this call is about to overwrite. Returns false on timeout (error word
 // set, block continues so the grid always drains).
 template <bool DATA = true, class V>
-__device__ __forceinline__ bool block_barrier(const V& v, uint32_t value) {
+__device__ __forceinline__ bool block_barrier(const V& v, uint32_t value, const PhaseTrace* tr = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   drain_vm();       // every storing wave drains its stores
   __syncthreads();  // ... before wave 0 publishes for the whole block
   bool ok = true;
   if (wave == 0) {
+    if (tr) tr->mark(13);
     if constexpr (DATA) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
       drain_vm();                                     // keep the wait after the fence (G16 pitfall 12)
@@ -508,6 +509,7 @@ __device__ __forceinline__ bool block_barrier(const V& v, uint32_t value) {
       uint32_t* f = v.flags[lane] + b * kern::kMaxRanks + v.rank;
       __hip_atomic_store(f, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (tr) tr->mark(14);
     const uint32_t* mine = v.flags[v.rank] + b * kern::kMaxRanks;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t it = 1;; ++it) {
@@ -529,6 +531,7 @@ __device__ __forceinline__ bool block_barrier(const V& v, uint32_t value) {
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    if (tr) tr->mark(15);
     if constexpr (DATA) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
       drain_vm();

@@ -128,8 +128,10 @@ using IpcView = IpcViewT<RawPtr>;
 // staged (a gated launch: its gate passed), [4] data barrier passed, [5] first pull / reduce done, [6] second data
 // barrier passed (2-shot), [7] exit; a gated zero-copy launch's device-side exchange (block 0):
 // [8] every rank's record in, [9] mapping lookup done, [10] every vote in, [11] verdict published.
+// [12] after the block's call number was taken, and inside the zero-copy arrival barrier: [13] every
+// wave drained (before the release), [14] flags stored to the peers, [15] every peer's flag seen.
 // Record `trace_slot` (one per launch, whatever the grid).
-constexpr int kTraceWords = 12;
+constexpr int kTraceWords = 16;
 // After the header, per block b < kTraceBlocks: [kTraceWords + b] the block's first pull /
 // reduce done ([5]), [kTraceWords + kTraceBlocks + b] its exit ([7]) -- how far the slowest
 // block trails block 0.

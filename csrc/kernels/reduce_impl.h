@@ -459,8 +459,8 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
   const size_t nt = c.bytes / kTile;
-  if (c.test_flags & 1) block_barrier<false>(v, ep);  // (measurement hook, see IpcCall::test_flags)
-  else block_barrier(v, ep);
+  if (c.test_flags & 1) block_barrier<false>(v, ep, &tr);  // (measurement hook, see IpcCall::test_flags)
+  else block_barrier(v, ep, &tr);
   tr.mark(2);
   tr.mark(4);
   if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
@@ -528,6 +528,7 @@ __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, 
   const int me = v.rank;
   const uint32_t seq = block_seq(v);
   tr.seq(seq);
+  tr.mark(12);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
   if (c.zc) {
     ipc_reduce_zc<DT, OP, W>(v, c, lds, tr, ep);

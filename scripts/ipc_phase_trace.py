@@ -64,7 +64,10 @@ def work(rank, size, mib, iters):
               "phase1_reduce": ph(4, 5), "barrier2": ph(5, 6), "phase2_gather": ph(6, 7), "kernel_total": ph(1, 7),
               # block 0's device-side buffer exchange of a gated zero-copy launch (words 8-11)
               "zx_records_in": ph(1, 8), "zx_lookup": ph(8, 9), "zx_votes_in": ph(9, 10), "zx_published": ph(10, 11),
-              "zx_to_arrival": ph(11, 2)}
+              "zx_to_arrival": ph(11, 2), "zx_to_args_staged": ph(11, 3), "args_staged_to_arrival": ph(3, 2),
+              # inside: call number taken, every wave drained, flags stored, every peer's flag seen
+              "block_seq": ph(3, 12), "barrier_drain": ph(12, 13), "barrier_store": ph(13, 14),
+              "barrier_poll": ph(14, 15), "barrier_acquire": ph(15, 2)}
     out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
            "phases_us": phases, "records": len(recs), "blocks_us": block_spread(recs)}
     # K1 at the same total workgroup budget: rank 0 alone, the others wait
@@ -88,7 +91,7 @@ def work(rank, size, mib, iters):
     return out
 
 
-HDR, NB = 12, 256  # kern::kTraceWords, kern::kTraceBlocks
+HDR, NB = 16, 256  # kern::kTraceWords, kern::kTraceBlocks
 
 
 def block_spread(recs):

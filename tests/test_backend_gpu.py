@@ -593,7 +593,7 @@ def test_phase_trace_records_every_block():
     # slowest block trails block 0 -- scripts/ipc_phase_trace.py blocks_us)
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_TRACE": "16", "PDCC_AUTOTUNE": "0"}
     for r in _gpu_launch(W.phase_trace_probe, 2, env=env, timeout_s=120):
-        assert r["ok"] and r["records"] >= 1 and r["rec_words"] == 12 + 2 * 256, r
+        assert r["ok"] and r["records"] >= 1 and r["rec_words"] == 16 + 2 * 256, r
         assert r["engine"].startswith("ipc_2shot"), r
         assert r["header_ordered"] and r["phase1_before_exit"], r
         assert r["blocks_exit"] >= 2 and r["blocks_phase1"] == r["blocks_exit"], r  # 256 / W blocks share one GPU
