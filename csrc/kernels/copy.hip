@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_copy_body<W>(sv, sc, lds, tr);
   tr.finish(v);
+  zx_publish_verdict(c);
 }
 
 }  // namespace dev

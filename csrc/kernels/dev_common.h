@@ -582,6 +582,11 @@ __device__ __forceinline__ void zx_put(uint64_t* p, uint32_t data, uint32_t tag)
   __hip_atomic_store(p, ((uint64_t)tag << 32) | data, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ __forceinline__ uint32_t& zx_verdict_note() {
+  __shared__ uint32_t s;
+  return s;
+}
+
 // Wave 0 of block 0: push {id, off} to every rank, collect every rank's, look the peers' ids
 // up in this process's mapping table, vote, and publish the verdict in this call's resolved
 // slot (ok = 1 with the buffers, 2 = wait for the host gate, 0 = a peer never came: staged,
@@ -716,10 +721,17 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
   tr.mark(11);
   if (lane == 0) {
     __hip_atomic_store(&res->seq, (c.zx_tag << 2) | verdict, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    // for the host's statistics (read when the gate slot is reused): a posted store, off the critical path
-    __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), 0x100u | verdict, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    zx_verdict_note() = 0x100u | verdict;  // for the host, written at the kernel's end (zx_publish_verdict)
   }
+}
+
+// The verdict for the host's statistics (read when the gate slot is reused). Stored to pinned host
+// memory only when block 0 is done: a store over PCIe stays outstanding for ~15 us, and the
+// block's next counted wait (its call-number load) would sit behind it on the critical path.
+__device__ __forceinline__ void zx_publish_verdict(const kern::IpcCall& c) {
+  if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), zx_verdict_note(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Thread 0 of every block: the resolved slot of this call (block 0 publishes it). Returns the

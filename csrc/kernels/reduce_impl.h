@@ -602,6 +602,7 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);
   tr.finish(v);
+  zx_publish_verdict(c);
 }
 
 // ----------------------------------------------------------------------------
