@@ -117,10 +117,11 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
 }
 
 template <int W>
-__device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr) {
+__device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
+                                              uint32_t seq0) {
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t seq = block_seq(v);
+  const uint32_t seq = block_seq(v, seq0);
   tr.seq(seq);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
   if (c.coll == IpcColl::BARRIER) {  // the arrival barrier is the whole collective
@@ -207,9 +208,10 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
+  const uint32_t seq0 = block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_copy_body<W>(sv, sc, lds, tr);
+  ipc_copy_body<W>(sv, sc, lds, tr, seq0);
   tr.finish(v);
   zx_publish_verdict(c);
 }

@@ -417,13 +417,20 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
 // counters[b], and consecutive launches on a stream run in order, so relaxed
 // accesses suffice (uncached signal memory: no stale line on any XCD); the store
 // is drained by the arrival barrier that follows.
+// The IPC kernels issue the load at entry (block_seq_load) and finish it after staging their
+// arguments (block_seq): an uncached load waits ~8 us behind the thread's older stores, and a
+// gated zero-copy launch's buffer exchange hides that wait.
 template <class V>
-__device__ __forceinline__ uint32_t block_seq(const V& v) {
+__device__ __forceinline__ uint32_t block_seq_load(const V& v) {
+  return threadIdx.x == 0 ? __hip_atomic_load(v.counters + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : 0u;
+}
+template <class V>
+__device__ __forceinline__ uint32_t block_seq(const V& v, uint32_t loaded) {
   __shared__ uint32_t s_seq;
   if (threadIdx.x == 0) {
-    uint32_t* const c = v.counters + blockIdx.x;
-    const uint32_t s = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-    __hip_atomic_store(c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t s = loaded + 1u;
+    __hip_atomic_store(v.counters + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq = s;
   }
   __syncthreads();

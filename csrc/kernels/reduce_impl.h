@@ -522,11 +522,12 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
 }
 
 template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr) {
+__device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
+                                                uint32_t seq0) {
   constexpr int D = DepthFor<W>::value;
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t seq = block_seq(v);
+  const uint32_t seq = block_seq(v, seq0);
   tr.seq(seq);
   tr.mark(12);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
@@ -598,9 +599,10 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
+  const uint32_t seq0 = block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr);
+  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq0);
   tr.finish(v);
   zx_publish_verdict(c);
 }
