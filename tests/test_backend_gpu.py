@@ -235,6 +235,7 @@ def test_group_churn_reuses_the_communicator(mode):
     (2, {"PDCC_ALGO": "ipc"}),                                 # IPC kernels, device-side sequence numbers
     (2, {}),                                                   # autotuned choices (host engine -> IPC)
     (3, {"PDCC_ALGO": "ipc", "PDCC_IPC_1SHOT_MAX": "0"}),      # 2-shot everywhere, partial rows
+    (2, {"PDCC_ALGO": "ipc_dyn", "PDCC_IPC_1SHOT_MAX": "64K"}),  # dynamic all-reduce: device-side epoch/counters
 ])
 def test_graph_capture_and_replay(world, env):
     for ok in _gpu_launch(W.graph_capture, world, env=env):
