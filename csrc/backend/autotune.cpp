@@ -39,9 +39,11 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   if (c == Coll::ALLREDUCE && cfg_.ipc_push && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
       bytes > cfg_.ipc_1shot_max)
     v.push_back(Algo::IPC_PUSH);
-  // the dynamic 2-shot all-reduce (zero-copy sizes): work items claimed per workgroup
-  if (c == Coll::ALLREDUCE && cfg_.ipc_dyn > 0 && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min &&
-      bytes > cfg_.ipc_1shot_max)
+  // the dynamic protocols (zero-copy sizes): work items claimed per workgroup -- the 2-shot
+  // all-reduce, the all-gather, the reduce-scatter
+  const bool dyn_coll = (c == Coll::ALLREDUCE && bytes > cfg_.ipc_1shot_max) || c == Coll::ALLGATHER ||
+                        c == Coll::REDUCE_SCATTER;
+  if (dyn_coll && cfg_.ipc_dyn > 0 && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min)
     v.push_back(Algo::IPC_DYN);
   return v;
 }

@@ -34,8 +34,10 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
       return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_PUSH : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_WIDE && ipc_can)  // only all_reduce races the wide grid
       return c == Coll::ALLREDUCE ? Algo::IPC_WIDE : Algo::IPC;
-    if (cfg_.force_algo == Algo::IPC_DYN && ipc_can)  // only the (zero-copy) all_reduce has it
-      return c == Coll::ALLREDUCE && ds.zc_ok ? Algo::IPC_DYN : Algo::IPC;
+    if (cfg_.force_algo == Algo::IPC_DYN && ipc_can)  // the zero-copy all_reduce / all_gather / reduce_scatter
+      return (c == Coll::ALLREDUCE || c == Coll::ALLGATHER || c == Coll::REDUCE_SCATTER) && ds.zc_ok
+                 ? Algo::IPC_DYN
+                 : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_STAGED && ipc_can) return Algo::IPC_STAGED;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
@@ -423,6 +425,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
       ic.launch(c, s);
       return;
     }
+    if (a == Algo::IPC_DYN && !rooted) c.dyn = std::max(1, cfg_.ipc_dyn);  // (zero-copy runs only)
     ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.chunk_cap(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
@@ -541,6 +544,7 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
       ic.launch(c, s);
       return;
     }
+    if (a == Algo::IPC_DYN) c.dyn = std::max(1, cfg_.ipc_dyn);  // (zero-copy runs only)
     // a flat input (reduce_scatter_tensor) is read in place by every peer
     ipc_run(ds, c, is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr, bytes * size_, kern::kTileBytes,
             ic.chunk_cap() / size_, s);
@@ -800,7 +804,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     icp = ds.ipc;
   }
   const bool ll = ds.ll_ok && bytes_in_ll_range(wi.nbytes());
-  const char* algo = is_ipc(a) ? (ll ? "ipc_ll" : "ipc")
+  const char* algo = is_ipc(a) ? (ll ? "ipc_ll" : a == Algo::IPC_DYN && !rooted ? "ipc_dyn" : "ipc")
                                     : (flat || rooted ? "rccl" : (cfg_.list_gather_p2p ? "rccl_p2p" : "rccl_staged"));
   auto work = gpu_issue(cname, ds, a, keep, co ? co->members : outs, to,
                         [=, dsp = &ds, outs = outs](hipStream_t x) mutable {
@@ -919,7 +923,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     if (!wo.is_same(out)) out.copy_(wo);
     if (co) co->run(x);
   }, icp);
-  record(Coll::REDUCE_SCATTER, is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : "ipc") : "rccl",
+  record(Coll::REDUCE_SCATTER,
+         is_ipc(a) ? (ds.ll_ok && bytes_in_ll_range(bytes) ? "ipc_ll" : a == Algo::IPC_DYN ? "ipc_dyn" : "ipc") : "rccl",
          bytes, t0);
   return work;
 }

@@ -365,28 +365,27 @@ __device__ __forceinline__ bool dyn_wait(const DView& v, const uint32_t* w, uint
 // positions I write in phase 2 (tile q + W*r of MY tensor) were read by q in its phase 1 of
 // chunk c, which q finished before publishing ready[c]; my own tiles are written in phase 1
 // only, and peers read them after my ready word.
-template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds) {
-  constexpr int D = DepthFor<W>::value;
-  const int me = v.rank;
-  const size_t nrows = c.bytes / kTile / W;
-  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn);
-  const uint32_t nc = (uint32_t)((nrows + K - 1) / K), total = nc * W;
-  uint32_t* const ctl = dyn_words(v, me, kern::kDynOffset);
-  uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
-  __shared__ uint32_t s_dep, s_item, s_ok;
-  if (threadIdx.x == 0) {  // this call's epoch (the previous dyn call's last block stored its own)
-    uint32_t e = __hip_atomic_load(ctl + kern::kDynEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+// This call's epoch: the previous dyn call's last block stored its own (never 0).
+__device__ __forceinline__ uint32_t dyn_epoch(const DView& v) {
+  __shared__ uint32_t s_dep;
+  if (threadIdx.x == 0) {
+    const uint32_t e = __hip_atomic_load(dyn_words(v, v.rank, kern::kDynOffset) + kern::kDynEpochWord,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_dep = e ? e : 1u;
   }
   __syncthreads();
-  const uint32_t dep = s_dep;
-  bool ok = true;
-  // Block b's first item is item b (no counter traffic at launch: every block hitting one uncached
-  // word at once serialises at the memory controller -- a fixed ~17 us at any size on one MI355X);
-  // later items are G + the counter. Thread 0 claims one item ahead, so the atomic's round trip
-  // overlaps the current item. Claims are monotonic (b < G <= G + k), so a held phase-1 item is
-  // never behind a phase-2 wait of the same block.
+  return s_dep;
+}
+
+// Claim loop: item(it) for every item this block claims, it < total. Block b's first item is item
+// b (no counter traffic at launch: every block hitting one uncached word at once serialises at the
+// memory controller -- a fixed ~17 us at any size on one MI355X); later items are G + the counter.
+// Thread 0 claims one item ahead, so the atomic's round trip overlaps the current item. Claims are
+// monotonic (b < G <= G + k): a block never holds an earlier item behind a later one.
+template <class Item>
+__device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, Item&& item) {
+  __shared__ uint32_t s_item;
+  uint32_t* const claim = dyn_words(v, v.rank, kern::kDynOffset) + kern::kDynClaimWord;
   uint32_t next = blockIdx.x;
   for (;;) {
     if (threadIdx.x == 0) s_item = next;
@@ -395,8 +394,47 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
     __syncthreads();  // (s_item is rewritten by the next claim)
     if (it >= total) break;
     if (threadIdx.x == 0)
-      next = gridDim.x +
-             __hip_atomic_fetch_add(ctl + kern::kDynClaimWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      next = gridDim.x + __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    item(it);
+  }
+}
+
+// Departure: once every block of mine is done (exit counter), the last one tells every peer, waits
+// until every peer's blocks are done too (nobody reads my tensor any more), then resets the counters
+// and publishes this call's epoch for the next dyn call.
+__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok) {
+  const int me = v.rank, W = v.world;
+  uint32_t* const ctl = dyn_words(v, me, kern::kDynOffset);
+  drain_vm();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(ctl + kern::kDynExitWord, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      for (int q = 0; q < W; ++q)
+        if (q != me)
+          __hip_atomic_store(dyn_words(v, q, kern::kDynDoneOffset) + me, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      uint32_t* const done = dyn_words(v, me, kern::kDynDoneOffset);
+      for (int q = 0; q < W; ++q)
+        if (q != me && ok) ok = dyn_wait(v, done + q, dep, 0x900u);
+      __hip_atomic_store(ctl + kern::kDynClaimWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + kern::kDynExitWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl + kern::kDynEpochWord, dep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <DType DT, RedOp OP, int W>
+__device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds) {
+  constexpr int D = DepthFor<W>::value;
+  const int me = v.rank;
+  const size_t nrows = c.bytes / kTile / W;
+  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn);
+  const uint32_t nc = (uint32_t)((nrows + K - 1) / K);
+  uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
+  __shared__ uint32_t s_ok;
+  const uint32_t dep = dyn_epoch(v);
+  bool ok = true;
+  dyn_claim_loop(v, nc * W, [&](uint32_t it) {
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
@@ -425,25 +463,26 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
         ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
       }
     }
-  }
-  // departure: once every block of mine is done, tell the peers; the last block waits until every
-  // peer's blocks are done too (nobody reads my tensor any more), then resets the counters
-  drain_vm();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(ctl + kern::kDynExitWord, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1) {
-      for (int q = 0; q < W; ++q)
-        if (q != me)
-          __hip_atomic_store(dyn_words(v, q, kern::kDynDoneOffset) + me, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      uint32_t* const done = dyn_words(v, me, kern::kDynDoneOffset);
-      for (int q = 0; q < W; ++q)
-        if (q != me && ok) ok = dyn_wait(v, done + q, dep, 0x900u);
-      __hip_atomic_store(ctl + kern::kDynClaimWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctl + kern::kDynExitWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ctl + kern::kDynEpochWord, dep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  });
+  dyn_depart(v, dep, ok);
+}
+
+// Dynamic zero-copy reduce-scatter (IpcCall::dyn): my output chunk in items of K tiles, each reduced
+// from every rank's flat input (chunk `me` at me * zstride) -- one phase, no ready words; the
+// departure keeps every peer's input alive until the last reader is done.
+template <DType DT, RedOp OP, int W>
+__device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCall& c, char* lds) {
+  constexpr int D = DepthFor<W>::value;
+  const size_t nt = c.bytes / kTile;
+  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn);
+  const uint32_t nc = (uint32_t)((nt + K - 1) / K);
+  const uint32_t dep = dyn_epoch(v);
+  dyn_claim_loop(v, nc, [&](uint32_t it) {
+    const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
+    const AllSrcMap<W> m{&v, (size_t)v.rank * c.zstride, (char*)c.out[0], c.bytes, t0, 1, t1};
+    ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
+  });
+  dyn_depart(v, dep, true);
 }
 
 // Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
@@ -465,6 +504,11 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   tr.mark(4);
   if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
     ipc_allreduce_dyn<DT, OP, W>(v, c, lds);
+    tr.mark(5);
+    return;
+  }
+  if (c.coll == IpcColl::REDUCE_SCATTER && c.dyn) {
+    ipc_reduce_scatter_dyn<DT, OP, W>(v, c, lds);
     tr.mark(5);
     return;
   }

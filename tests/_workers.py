@@ -1793,6 +1793,10 @@ def dyn_stress(rank, size, device="cuda", calls=60):
     sizes = [(1 << 20) // 4, (8 << 20) // 4 + 3, (64 << 20) // 4, (3 << 20) // 4 + 1024]
     bufs = [torch.empty(n, device=d) for n in sizes]
     small = torch.empty(1000, device=d)
+    ag_in = torch.empty((4 << 20) // 4, device=d)
+    ag_out = torch.empty(size * ag_in.numel(), device=d)
+    rs_in = torch.empty(size * ((4 << 20) // 4), device=d)
+    rs_out = torch.empty((4 << 20) // 4, device=d)
     ok, engines = True, set()
     for i in range(calls):
         x = bufs[i % len(bufs)]
@@ -1808,6 +1812,16 @@ def dyn_stress(rank, size, device="cuda", calls=60):
             small.fill_(1.0)
             dist.all_reduce(small)
             ok = ok and bool(torch.all(small == size))
+        if i % 4 == 1:  # the dynamic all-gather and reduce-scatter (4 MiB per rank)
+            ag_in.fill_(float(rank + i))
+            dist.all_gather_into_tensor(ag_out, ag_in)
+            engines.add(b.last_algo())
+            want_ag = torch.arange(size, device=d, dtype=torch.float32).repeat_interleave(ag_in.numel()) + i
+            ok = ok and bool(torch.equal(ag_out, want_ag))
+            rs_in.fill_(float(rank + 1 + i % 3))
+            dist.reduce_scatter_tensor(rs_out, rs_in)
+            engines.add(b.last_algo())
+            ok = ok and bool(torch.all(rs_out == float(sum(r + 1 + i % 3 for r in range(size)))))
         if i % 11 == 10:
             dist.barrier()
     torch.cuda.synchronize()
