@@ -185,6 +185,20 @@ struct OneSrcMap {  // copy tile t from one buffer to another
 
 constexpr int kCopyDepth = 4;
 
+// The zero-copy all-reduce's pipes. PDCC_TEST_IPC_FLAGS (IpcCall::test_flags, A/B measurements only):
+// bit 1 = non-temporal loads and stores in the gather phase (tiles read once, written once), bit 2 =
+// non-temporal stores in the reduce phase.
+template <class Map>
+__device__ __forceinline__ void zc_copy_pipe(char* lds, const Map& m, int flags) {
+  if (flags & 2) pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, Map, 1, true, true>(lds, m, 1);
+  else ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+}
+template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
+__device__ __forceinline__ void zc_reduce_pipe(char* lds, const Map& m, int avg_div, int flags) {
+  if (flags & 4) pipe_run<DT, OP, NSRC, DEPTH, Map, 1, true, PDCC_IPC_ZC_NTL != 0>(lds, m, avg_div);
+  else ipc_pipe_once<DT, OP, NSRC, DEPTH>(lds, m, avg_div);
+}
+
 // Owner-interleaved maps. A block's pipeline keeps DEPTH tiles in flight; if all
 // of them (and, with blocks in lockstep, all blocks of the rank) pull from the
 // same peer, a rank drives ONE xGMI link at a time. These maps rotate the owner
@@ -438,7 +452,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
-      ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
+      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div, c.test_flags);
       drain_vm();  // every wave's stores and loads (a peer overwrites what I read once it sees ready)
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -460,7 +474,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
       if (ok) {
         const size_t r0 = (size_t)cc * K, r1 = r0 + K < nrows ? r0 + K : nrows;
         const OneSrcMap m{v.buf[q], v.buf[me], c.bytes, (size_t)q + W * r0, W, W * r1};
-        ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+        zc_copy_pipe(lds, m, c.test_flags);
       }
     }
   });
@@ -515,14 +529,14 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
     {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
+      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div, c.test_flags);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
     tr.mark(6);
     {  // phase 2: the other owners' reduced tiles
       const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
-      ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+      zc_copy_pipe(lds, m, c.test_flags);
     }
   } else if (c.coll == IpcColl::ALLREDUCE_PUSH) {
     // every remote access is a write (xGMI writes are posted; reads wait a round trip)
