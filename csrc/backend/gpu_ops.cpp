@@ -1167,6 +1167,14 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::endCoalescing() {
   coalesced_cpu_.clear();
   for (auto& w : cpu_works) w->wait();
   if (!ds) return cpu_done(Coll::SEND, {});
+  // nothing was batched (torch's fast path issued one coalesced collective instead): a synchronous
+  // one already ran on the caller's stream, so there is nothing to order -- an async one ran on the
+  // comm stream and the returned work must cover it (below)
+  if (coalesced_.empty() && !op_async_) {
+    coalesced_tensors_.clear();
+    coalesced_ds_ = nullptr;
+    return cpu_done(Coll::SEND, {});
+  }
   auto fns = std::move(coalesced_);
   auto keep = std::move(coalesced_tensors_);
   coalesced_.clear();
