@@ -188,10 +188,17 @@ constexpr int kCopyDepth = 4;
 // The zero-copy all-reduce's pipes. PDCC_TEST_IPC_FLAGS (IpcCall::test_flags, A/B measurements only):
 // bit 1 = non-temporal loads and stores in the gather phase (tiles read once, written once), bit 2 =
 // non-temporal stores in the reduce phase.
+// The gather phase runs in the reduce kernels, whose LDS is sized for the reduce pipe (W x
+// DepthFor<W> tiles, >= 32 KiB for every W): the copy keeps 8 tiles in flight instead of 4 there
+// (Little's law: the bytes in flight per workgroup set a streaming copy's rate).
+constexpr int kZcCopyDepth = 8;
+static_assert(2 * DepthFor<2>::value >= kZcCopyDepth && 3 * DepthFor<3>::value >= kZcCopyDepth &&
+                  5 * DepthFor<5>::value >= kZcCopyDepth,
+              "the reduce kernels' LDS must hold the gather phase's ring");
 template <class Map>
 __device__ __forceinline__ void zc_copy_pipe(char* lds, const Map& m, int flags) {
-  if (flags & 2) pipe_run<DType::U8, RedOp::COPY, 1, kCopyDepth, Map, 1, true, true>(lds, m, 1);
-  else ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
+  if (flags & 2) pipe_run<DType::U8, RedOp::COPY, 1, kZcCopyDepth, Map, 1, true, true>(lds, m, 1);
+  else ipc_pipe<DType::U8, RedOp::COPY, 1, kZcCopyDepth>(lds, m, 1);
 }
 template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
 __device__ __forceinline__ void zc_reduce_pipe(char* lds, const Map& m, int avg_div, int flags) {
