@@ -40,6 +40,12 @@ sys.path.insert(0, ROOT)
 BASELINE_BUSBW = {2: 6.14, 4: 5.49, 8: 3.16}  # BASELINE.md §2.1 (reference stack, Gloo/CPU)
 BASELINE_P50_MS = {1: 0.027, 2: 174.8, 4: 293.4, 8: 595.1}  # same table, p50 latency
 SMALL = os.environ.get("PDCC_BENCH_SMALL", "0") == "1"  # functional rehearsal sizes for the extras
+# PDCC_BENCH_RCCL_REHEARSAL=1 (world 1, one GPU): run the RCCL-only extras the driver's multi-GPU
+# node would run first -- the RCCL environment pre-sweep in fresh child ranks, torch's own
+# ProcessGroupNCCL comparator, the RCCL A/B, the baseline rows, the CTA sweep / list all-gather /
+# group churn -- on 1-rank communicators (PDCC_WORLD1_LOCAL=0: the library's RCCL engine runs even
+# where all_reduce is a no-op), so none of them first executes on the scaling run
+REHEARSAL = os.environ.get("PDCC_BENCH_RCCL_REHEARSAL", "0") == "1"
 NBYTES = 1 << 30
 EXTRAS_PARTIAL: dict = {}  # run_extras fills this in place (reported even if a deadline fires)
 # wall seconds per section of this rank's run (extras.timing; rank 0's view): on the first
@@ -162,6 +168,10 @@ def run_rank(args):
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     on_gpu = os.environ.get("PDCC_BENCH_DEVICE", "cuda") != "cpu"
+    if REHEARSAL:
+        if world != 1 or not on_gpu:
+            raise SystemExit("PDCC_BENCH_RCCL_REHEARSAL=1 is a world-1 GPU rehearsal (--gpus 1)")
+        os.environ["PDCC_WORLD1_LOCAL"] = "0"  # before the pre-sweep's children and our own group
     TIMING["startup"] = round(time.time() - T_START, 3)
     if world == 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -292,8 +302,10 @@ def run_rank(args):
             "correct": correct,
             "data_finite": finite,
             # torch's own ProcessGroupNCCL on the same 1 GiB all_reduce (extras.torch_nccl): its p50 / ours
-            "vs_torch_nccl": _vs_torch_nccl_headline(extras, p50),
-            "note": "world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition" if world == 1 else "",
+            "vs_torch_nccl": _vs_torch_nccl_headline(extras, p50, args.bytes),
+            "note": ("world=1: all_reduce is a no-op, busbw is 0 by the nccl-tests definition"
+                     + ("; RCCL rehearsal (1-rank communicators, PDCC_WORLD1_LOCAL=0)" if REHEARSAL else ""))
+                    if world == 1 else "",
             "extras": extras,
         }
 
@@ -351,7 +363,7 @@ def rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args):
     rank's own communicators (every rank applies the same one). Distinct GPUs only."""
     if not on_gpu:
         return {"skipped": "CPU rehearsal (PDCC_BENCH_DEVICE=cpu)"}
-    if world < 2:
+    if world < 2 and not REHEARSAL:
         return {"skipped": "world=1: no communicator to tune"}
     if ngpu < world:
         return {"skipped": f"ranks share a GPU ({world} ranks, {ngpu} GPU): RCCL refuses duplicate devices"}
@@ -364,7 +376,7 @@ def rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args):
     if rank == 0:
         print("[bench] RCCL environment pre-sweep (fresh child ranks per point)", file=sys.stderr, flush=True)
     try:
-        rec, env = rccl_env.sweep(store, rank, world, local, nbytes=args.bytes if not SMALL else 64 << 20,
+        rec, env = rccl_env.sweep(store, rank, world, local, nbytes=min(args.bytes, 64 << 20) if SMALL else args.bytes,
                                   budget_s=float(os.environ.get("PDCC_BENCH_RCCL_ENV_SWEEP_S", "90")))
     except Exception as e:  # never in the way of the headline
         return {"error": f"{type(e).__name__}: {e}"[:300]}
@@ -398,10 +410,11 @@ def run_extras(world, rank, dev, native, x):
     out = EXTRAS_PARTIAL  # filled in place, so a deadline still reports what finished
     with section("k1"):
         run_k1(world, dev, out)
-    if world == 1:
+    if world == 1 and not REHEARSAL:
         out["torch_nccl"] = {"skipped": "world=1: all_reduce is a no-op"}
         return out
-    out["links"] = link_summary(world)
+    if world > 1:
+        out["links"] = link_summary(world)
     # torch's own ProcessGroupNCCL over the same RCCL first: the bar this library must beat
     with section("torch_nccl"):
         try:
@@ -425,11 +438,12 @@ def run_extras(world, rank, dev, native, x):
                 out["rccl_tuning"] = rccl_tuning(world, rank, dev, x)
             except Exception as e:
                 out["rccl_tuning_error"] = f"{type(e).__name__}: {e}"[:300]
-        with section("ipc_grid_sweep"):
-            try:
-                out["ipc_grid_sweep_allreduce_busbw"] = ipc_grid_sweep(world, rank, dev, x)
-            except Exception as e:
-                out["ipc_grid_sweep_error"] = f"{type(e).__name__}: {e}"[:300]
+        if world > 1:  # (the IPC engines need peers)
+            with section("ipc_grid_sweep"):
+                try:
+                    out["ipc_grid_sweep_allreduce_busbw"] = ipc_grid_sweep(world, rank, dev, x)
+                except Exception as e:
+                    out["ipc_grid_sweep_error"] = f"{type(e).__name__}: {e}"[:300]
     return out
 
 
@@ -473,9 +487,11 @@ def algo_ab(world, rank, dev, native, x, out):
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         return f.item() > 0
 
-    big = (1 << 30) if not SMALL else (64 << 20)
+    big = min((1 << 30) if not SMALL else (64 << 20), x.numel() * 4)
     rccl_ok = "rccl_ok=1" in native.describe()
     algos = ("rccl", "ipc", "ipc_push", "ipc_dyn") if rccl_ok else ("ipc", "ipc_push", "ipc_dyn")
+    if world == 1:  # RCCL rehearsal: no IPC engine at world 1
+        algos = ("rccl", "rccl_wide")
     if not rccl_ok:
         out["rccl_rows"] = "dropped: ranks share a GPU, RCCL unavailable"
     for algo in algos:
@@ -740,48 +756,53 @@ def baseline_configs(world, rank, dev, x, group=None, engine=None):
         progress(name if engine is None else f"{engine}: {name}")
         t = _p50_coll(fn, iters)
         res[name] = {"p50_ms": round(t * 1e3, 3), "busbw_GBps": round(bb(coll, total_bytes, world, t), 1),
-                     "engine": engine or _p50_coll.engine}
+                     "bytes": total_bytes, "engine": engine or _p50_coll.engine}
         if check is not None:
             res[name]["correct"] = bool(check())
 
     try:
-        S = 1 << 30 if not SMALL else 64 << 20
+        # row names carry the size actually timed (SMALL rehearsals: 64 MiB, not 1 GiB)
+        S = min(1 << 30 if not SMALL else 64 << 20, x.numel() * 4)
+        L = size_label(S)
         n = S // 4
         chunk = n // world
-        x.uniform_(0.0, 1e-3)
-        rec("all_reduce_1GiB", "all_reduce", S, lambda: dist.all_reduce(x, group=g))
-        rec("reduce_1GiB", "reduce", S, lambda: dist.reduce(x, dst=0, group=g))
-        rec("broadcast_1GiB", "broadcast", S, lambda: dist.broadcast(x, src=0, group=g))
+        xs = x[:n]
+        xs.uniform_(0.0, 1e-3)
+        rec(f"all_reduce_{L}", "all_reduce", S, lambda: dist.all_reduce(xs, group=g))
+        rec(f"reduce_{L}", "reduce", S, lambda: dist.reduce(xs, dst=0, group=g))
+        rec(f"broadcast_{L}", "broadcast", S, lambda: dist.broadcast(xs, src=0, group=g))
         src = torch.full((chunk,), float(rank), device=dev)
         out = torch.empty(n - n % world, device=dev)
-        rec("all_gather_1GiB", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src, group=g),
+        rec(f"all_gather_{L}", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src, group=g),
             check=lambda: torch.equal(out.view(world, chunk)[:, 0].cpu(), torch.arange(world, dtype=torch.float32)))
         glist = [torch.empty(chunk, device=dev) for _ in range(world)] if rank == 0 else None
-        rec("gather_1GiB", "gather", S, lambda: dist.gather(src, gather_list=glist, dst=0, group=g),
+        rec(f"gather_{L}", "gather", S, lambda: dist.gather(src, gather_list=glist, dst=0, group=g),
             check=lambda: rank != 0 or all(bool(glist[r][0].item() == r) for r in range(world)))
         slist = [torch.full((chunk,), float(r), device=dev) for r in range(world)] if rank == 0 else None
         sout = torch.empty(chunk, device=dev)
-        rec("scatter_1GiB", "scatter", S, lambda: dist.scatter(sout, scatter_list=slist, src=0, group=g),
+        rec(f"scatter_{L}", "scatter", S, lambda: dist.scatter(sout, scatter_list=slist, src=0, group=g),
             check=lambda: sout[0].item() == rank)
         del glist, slist
         rsin = torch.ones(n - n % world, device=dev)
-        rec("reduce_scatter_1GiB", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin, group=g),
+        rec(f"reduce_scatter_{L}", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin, group=g),
             check=lambda: sout[0].item() == world)
         a2a = torch.empty_like(rsin)
-        rec("all_to_all_1GiB", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin, group=g))
+        rec(f"all_to_all_{L}", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin, group=g))
         del rsin, a2a, out, src
         m = ((128 << 20) if not SMALL else (8 << 20)) // 4
         for op in ("PRODUCT", "MAX", "MIN"):
             v = torch.full((m,), 1.0 + 1e-7 * rank, device=dev)
-            rec(f"all_reduce_{op}_128MiB", "all_reduce", m * 4,
+            rec(f"all_reduce_{op}_{size_label(m * 4)}", "all_reduce", m * 4,
                 lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op), group=g))
         del v
         if world == 2:
-            rec("all_reduce_256MiB", "all_reduce", 256 << 20, lambda: dist.all_reduce(x[: (256 << 20) // 4], group=g))
+            n2 = min(256 << 20, x.numel() * 4) // 4
+            rec(f"all_reduce_{size_label(n2 * 4)}_w2", "all_reduce", n2 * 4,
+                lambda: dist.all_reduce(x[:n2], group=g))
         per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
         ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)
         ag_out = torch.empty(per * world, dtype=torch.bfloat16, device=dev)
-        rec("all_gather_bf16_4GiB_per_rank", "all_gather", per * 2 * world,
+        rec(f"all_gather_bf16_{size_label(per * 2)}_per_rank", "all_gather", per * 2 * world,
             lambda: dist.all_gather_into_tensor(ag_out, ag_in, group=g), iters=3,
             check=lambda: torch.equal(ag_out.view(world, per)[:, -1].float().cpu(),
                                       torch.arange(world, dtype=torch.float32)))
@@ -812,10 +833,19 @@ def torch_nccl_compare(world, rank, dev, native, x):
     return {"rows": rows}
 
 
-def _vs_torch_nccl_headline(extras, p50_s):
+def size_label(nbytes: int) -> str:
+    """1073741824 -> '1GiB', 67108864 -> '64MiB' (row names carry the size they time)."""
+    for unit, shift in (("GiB", 30), ("MiB", 20), ("KiB", 10)):
+        if nbytes >= (1 << shift) and nbytes % (1 << shift) == 0:
+            return f"{nbytes >> shift}{unit}"
+    return f"{nbytes}B"
+
+
+def _vs_torch_nccl_headline(extras, p50_s, nbytes):
+    """torch's p50 / ours for the headline all_reduce, if the comparator timed that same size."""
     try:
-        row = extras["torch_nccl"]["rows"]["all_reduce_1GiB"]
-        return round(row["p50_ms"] / (p50_s * 1e3), 3) if p50_s > 0 and not SMALL else None
+        row = extras["torch_nccl"]["rows"][f"all_reduce_{size_label(nbytes)}"]
+        return round(row["p50_ms"] / (p50_s * 1e3), 3) if p50_s > 0 else None
     except (KeyError, TypeError):
         return None
 

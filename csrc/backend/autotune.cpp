@@ -21,9 +21,13 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
   // LL sizes keep the static choice: a race there would time the LL kernel and then apply
   // the verdict to the staged protocol the rest of the power-of-two bucket takes
   if (ll_can && bytes_in_ll_range(bytes)) return v;
-  if (rccl_can) v.push_back(Algo::RCCL);                       // reference engine
-  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);     // no RCCL (ranks share a GPU)
-  else return {};
+  // reference engine: RCCL; without it (ranks sharing a GPU, or a reduction RCCL lacks:
+  // BAND/BOR/BXOR, integer AVG) the host transport for small keys, and above kHostTuneMax the
+  // static IPC engine itself -- checked against the host transport on a <= kHostTuneMax
+  // prefix of the caller's data once per key (autotune(): `ref_check`) -- so the IPC variants
+  // are still raced where the host path is too slow to time against
+  if (rccl_can) v.push_back(Algo::RCCL);
+  else if (bytes <= kHostTuneMax) v.push_back(Algo::HOST);
   // RCCL with more channels than its topology tuner picks (large all_reduce keys)
   if (c == Coll::ALLREDUCE && rccl_can && cfg_.rccl_wide_ctas > 0 && bytes >= cfg_.rccl_wide_min)
     v.push_back(Algo::RCCL_WIDE);
@@ -45,6 +49,7 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
                         c == Coll::REDUCE_SCATTER;
   if (dyn_coll && cfg_.ipc_dyn > 0 && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min)
     v.push_back(Algo::IPC_DYN);
+  if (v.size() < 2) return {};  // nothing to race
   return v;
 }
 
@@ -61,11 +66,15 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
                                 bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
   const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok, ds.ll_ok);
   if (cands.empty()) return a0;
-  const TuneKey key{(int)c, dtype, op, size_bucket(bytes)};
+  // an async call whose IPC launches run the capped grid (PDCC_IPC_ASYNC_GRID) is a key of its own
+  // (bucket + kAsyncBucket): a verdict timed at one grid is never applied at the other
+  const int bucket = size_bucket(bytes) + (op_async_ && cfg_.ipc_async_grid > 0 ? kAsyncBucket : 0);
+  const TuneKey key{(int)c, dtype, op, bucket};
   const Algo t = tuned(key);
   const bool cap = capturing_on(ds.device);
   if (t != Algo::AUTO) {
-    if (std::find(cands.begin(), cands.end(), t) == cands.end()) return a0;
+    // (HOST also stands for "the IPC reference engine failed its host check": always feasible)
+    if (t != Algo::HOST && std::find(cands.begin(), cands.end(), t) == cands.end()) return a0;
     if (t == Algo::HOST && cap) return Algo::IPC;  // tuned to the host engine, which cannot be captured
     return t;
   }
@@ -97,7 +106,8 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
 
 Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
                                   const std::function<void(size_t)>& run,
-                                  const std::function<bool(size_t, size_t)>& same) {
+                                  const std::function<bool(size_t, size_t)>& same,
+                                  const std::function<bool()>& ref_check) {
   c10::hip::HIPGuardMasqueradingAsCUDA g((c10::DeviceIndex)ds.device);
   const hipStream_t s = current_stream(ds.device);
   const size_t n = cands.size();
@@ -127,6 +137,35 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   // an async call's key is raced with the grid its IPC launches will run at (PDCC_IPC_ASYNC_GRID):
   // the verdict must hold for the capped engine next to compute, not for the full grid
   IpcComm::AsyncScope async_cap(has_ipc ? ds.ipc.get() : nullptr, op_async_ && cfg_.ipc_async_grid > 0);
+  // The IPC engine as the reference (no RCCL, above kHostTuneMax): first its result on a prefix
+  // of the caller's data against the host transport's, agreed on every rank. A failure (or an
+  // IPC spin timeout in the reference run below) sends the key to the host engine: slow, exact.
+  auto host_fallback = [&](const char* why) {
+    if (ds.ipc) ds.ipc->clear_error();
+    fprintf(stderr, "[pdcc r%d] autotune %s %zu B: reference IPC engine %s; using the host engine for this key\n",
+            rank_, coll_name((Coll)std::get<0>(key)), bytes, why);
+    TuneEntry te;
+    te.ref = cands[0];
+    te.valid = false;
+    te.algo = Algo::HOST;
+    std::lock_guard<std::mutex> lk(tune_mu_);
+    tune_[key] = te;
+    return Algo::HOST;
+  };
+  const bool ipc_ref = is_ipc(cands[0]);
+  if (ipc_ref && ref_check) {
+    bool ok = false;
+    try {
+      ok = ref_check();
+      PDCC_HIP(hipStreamSynchronize(s));
+      ok = ok && !(ds.ipc && ds.ipc->error_word() != 0);
+    } catch (const std::exception& e) {
+      ok = false;
+    }
+    double f = ok ? 1.0 : 0.0;
+    shm().allreduce(&f, 1, at::kDouble, RedOpType::MIN, timeout_);
+    if (f <= 0.0) return host_fallback("disagrees with the host transport on a prefix");
+  }
   // 0) warm-up: one run each (staging growth, first-touch), then check every result
   //    against the reference engine's on identical data
   for (size_t k = 0; k < n; ++k) {
@@ -141,6 +180,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   PDCC_HIP(hipStreamSynchronize(s));
   std::vector<double> v(2 * n, 0.0);  // [estimate_us x n, mismatch x n], MAX-reduced across ranks
   const bool ipc_fault = has_ipc && ds.ipc && ds.ipc->error_word() != 0;
+  if (ipc_ref && ipc_fault) v[n] = 2.0;  // the reference itself timed out
   for (size_t k = 1; k < n; ++k)
     v[n + k] = (is_ipc(cands[k]) && ipc_fault) ? 2.0 : (same(0, k) ? 0.0 : 1.0);
   {  // agree on faults first (every rank's stream is drained: no IPC kernel is running)
@@ -148,6 +188,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     shm().allreduce(f.data(), f.size(), at::kDouble, RedOpType::MAX, timeout_);
     std::copy(f.begin(), f.end(), v.begin() + n);
   }
+  if (v[n] >= 2.0) return host_fallback("timed out");
   std::vector<bool> live(n, true);
   for (size_t k = 1; k < n; ++k)
     if (v[n + k] >= 2.0) {
@@ -201,6 +242,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   te.ref = cands[0];
   te.iters = iters;
   te.valid = true;
+  te.rccl_us = med[0];  // the reference engine's time (RCCL, the host transport, or static IPC)
   for (size_t k = 0; k < n; ++k) {
     if (is_ipc(cands[k])) {
       (cands[k] == Algo::IPC          ? te.ipc_us
@@ -212,8 +254,6 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
     } else if (cands[k] == Algo::RCCL_WIDE) {
       te.wide_us = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
-    } else {
-      te.rccl_us = med[k];  // the reference engine (RCCL, or the host transport without RCCL)
     }
   }
   te.algo = cands[best];
@@ -279,8 +319,8 @@ void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, con
   std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
                "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f, ipc_dyn %.1f\n",
                tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
-               algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref), (size_t)1 << std::get<3>(key),
-               (size_t)2 << std::get<3>(key), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us,
+               algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref),
+               (size_t)1 << (std::get<3>(key) % kAsyncBucket), (size_t)2 << (std::get<3>(key) % kAsyncBucket), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us,
                e.dyn_us);
   std::fflush(f);
   flock(fileno(f), LOCK_UN);
@@ -292,7 +332,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
   std::vector<TuneRecord> out;
   for (const auto& kv : tune_) {
     const TuneEntry& e = kv.second;
-    const int dt = std::get<1>(kv.first), op = std::get<2>(kv.first), b = std::get<3>(kv.first);
+    const int dt = std::get<1>(kv.first), op = std::get<2>(kv.first), b = std::get<3>(kv.first) % kAsyncBucket;
     TuneRecord r;
     r.coll = coll_name((Coll)std::get<0>(kv.first));
     r.dtype = dt < 0 ? "-" : c10::toString((at::ScalarType)dt);
@@ -310,6 +350,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.valid = e.valid;
     r.algo = algo_name(e.algo);
     r.iters = e.iters;
+    r.async_capped = std::get<3>(kv.first) >= kAsyncBucket;
     out.push_back(r);
   }
   return out;

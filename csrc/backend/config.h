@@ -67,7 +67,11 @@ struct Config {
   // ranks on one MI355X (profiles/r4/zero_bench_async_grid_r4.jsonl): replicated DP 36.4-36.7 ms at 64
   // vs 37.2-37.5 uncapped, ZeRO 30.8-31.2 either way, 32 worse; 64 workgroups still keep ~4 MiB of
   // remote loads in flight per GPU at W = 8 -- about RCCL's own CTA footprint for a collective.
-  int ipc_async_grid = 64;                 // PDCC_IPC_ASYNC_GRID
+  // OPT-IN (default 0): the grid then depends on each rank's own async_op, which torch treats as
+  // rank-local; the block-pairwise protocol needs the same grid on every rank, so with a cap set
+  // every rank must pass the same async_op to each collective (DDP / ZeRO buckets do). PDCC_DEBUG=1
+  // checks that per call; the autotuner keys capped (async) calls separately from full-grid ones.
+  int ipc_async_grid = 0;                  // PDCC_IPC_ASYNC_GRID
   // Zero-copy calls exchange their records on a per-device launcher thread (IpcLauncher in
   // process_group.h): the caller's host never waits for its peers (0 = inline exchange)
   bool ipc_zc_async = true;                // PDCC_IPC_ZC_ASYNC

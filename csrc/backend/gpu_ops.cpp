@@ -230,8 +230,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
   {
     c10::hip::HIPStreamGuardMasqueradingAsCUDA sg(comm);  // temporaries + copy-backs run on the comm stream
     // an async collective (comm stream) runs next to the caller's compute: its IPC launches
-    // take at most PDCC_IPC_ASYNC_GRID workgroups
-    IpcComm::AsyncScope as(ipcp.get(), comm != cur && !stream);
+    // take at most PDCC_IPC_ASYNC_GRID workgroups (async_op=True only: PDCC_STREAM=comm puts
+    // synchronous calls on the comm stream too, and those keep the full grid)
+    IpcComm::AsyncScope as(ipcp.get(), op_async_ && comm != cur && !stream);
     fn(comm.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
@@ -673,7 +674,15 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
     return autotune(
         key, bytes, ds, cands,
         [&](size_t k) { enqueue_allreduce(cands[k], sc[k], kd, ko, nd, no, nok, op, root, rooted, ds, cs, to); },
-        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); });
+        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); },
+        [&] {  // IPC as the reference: itself vs the host transport on a prefix
+          const int64_t m = sample_numel(w.numel(), w.element_size(), kHostTuneMax);
+          at::Tensor h = w.reshape({-1}).narrow(0, 0, m).clone(), g = h.clone();
+          enqueue_allreduce(Algo::HOST, h, kd, ko, nd, no, nok, op, root, rooted, ds, cs, to);
+          enqueue_allreduce(cands[0], g, kd, ko, nd, no, nok, op, root, rooted, ds, cs, to);
+          PDCC_HIP(hipStreamSynchronize(cs));
+          return results_match(h, g, op, size_);
+        });
   });
   if (a == Algo::HOST) {
     enqueue_allreduce(Algo::HOST, w, kd, ko, nd, no, nok, op, root, rooted, ds, current_stream(ds.device), to);
@@ -900,7 +909,16 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
     return autotune(
         key, bytes, ds, cands,
         [&](size_t k) { enqueue_reduce_scatter(cands[k], si, sc[k], kd, ko, nd, no, nok, op, ds, cs, to); },
-        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); });
+        [&](size_t r, size_t k) { return results_match(sc[r], sc[k], op, size_); },
+        [&] {  // IPC as the reference: itself vs the host transport on a prefix of every chunk
+          const int64_t m = sample_numel(wo.numel(), wo.element_size(), kHostTuneMax, size_);
+          const std::vector<at::Tensor> pi = sample_inputs(wi, m, false);
+          at::Tensor h = at::empty({m}, wo.options()), g = at::empty({m}, wo.options());
+          enqueue_reduce_scatter(Algo::HOST, pi, h, kd, ko, nd, no, nok, op, ds, cs, to);
+          enqueue_reduce_scatter(cands[0], pi, g, kd, ko, nd, no, nok, op, ds, cs, to);
+          PDCC_HIP(hipStreamSynchronize(cs));
+          return results_match(h, g, op, size_);
+        });
   });
   if (a == Algo::HOST) {
     enqueue_reduce_scatter(Algo::HOST, wi, wo, kd, ko, nd, no, nok, op, ds, current_stream(ds.device), to);

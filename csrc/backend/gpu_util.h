@@ -18,8 +18,6 @@
 
 #include "../device/comm_util.h"
 #include "process_group.h"
-#include "../device/comm_util.h"
-#include "process_group.h"
 
 namespace pdcc {
 namespace gpu {
@@ -139,6 +137,8 @@ inline void multi_copy_or_memcpy(const std::vector<kern::CopyDesc>& d, hipStream
 }
 
 inline int size_bucket(size_t bytes) { return bytes ? 63 - __builtin_clzll((unsigned long long)bytes) : 0; }
+// tune-key size slot of an async_op call whose IPC launches run the capped grid: bucket + this
+constexpr int kAsyncBucket = 64;
 
 // is `s` being captured into a graph (torch.cuda.graph / parallel.graphs)?
 inline bool capturing(hipStream_t s) {

@@ -202,7 +202,7 @@ void WorkMI355X::check_health() {
     throw std::runtime_error("pdcc: process group is in an error state: " + health_->message());
   if (ipc_ && ipc_->error_word() != 0)
     throw std::runtime_error("pdcc: an IPC collective timed out waiting for a peer (error word " +
-                             std::to_string(ipc_->error_word()) + ")");
+                             IpcComm::describe_error(ipc_->error_word()) + ")");
   std::lock_guard<std::mutex> lk(mutex_);
   if (exception_) std::rethrow_exception(exception_);
 }
@@ -517,7 +517,7 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
     int32_t coll, dtype;
     int64_t numel;
     int32_t root, dev_type;
-    int32_t async_op, pad;  // async collectives may run capped grids (PDCC_IPC_ASYNC_GRID): ranks must agree
+    int32_t async_op, pad;  // with PDCC_IPC_ASYNC_GRID set, async collectives run capped grids: ranks must agree
   };
   Fp mine{op_seq_.load(), (int32_t)c, ts.empty() ? -1 : (int32_t)ts[0].scalar_type(),
           ts.empty() ? 0 : ts[0].numel(), root, ts.empty() ? -1 : (int32_t)ts[0].device().type(),
@@ -530,7 +530,7 @@ void ProcessGroupMI355X::debug_check(Coll c, const std::vector<at::Tensor>& ts, 
     const Fp& f = all[r];
     if (f.seq != mine.seq || f.coll != mine.coll || f.dtype != mine.dtype || f.numel != mine.numel ||
         f.root != mine.root || f.dev_type != mine.dev_type ||
-        (f.async_op != mine.async_op && mine.dev_type == (int32_t)c10::DeviceType::CUDA)) {
+        (f.async_op != mine.async_op && cfg_.ipc_async_grid > 0 && mine.dev_type == (int32_t)c10::DeviceType::CUDA)) {
       std::ostringstream o;
       o << "pdcc DEBUG: collective mismatch at op #" << mine.seq << ": rank " << rank_ << " runs "
         << coll_name(c) << "(dtype=" << mine.dtype << ", numel=" << mine.numel << ", root=" << mine.root
@@ -823,7 +823,7 @@ void ProcessGroupMI355X::watchdog_loop() {
       }
       if (ds.ipc && ds.ipc->error_word() != 0 && !health_->poisoned.load() && !tuning_.load()) {
         const std::string m = "IPC collective timed out waiting for a peer (error word " +
-                              std::to_string(ds.ipc->error_word()) + ")";
+                              IpcComm::describe_error(ds.ipc->error_word()) + ")";
         fprintf(stderr, "[pdcc] rank %d: %s\n", rank_, m.c_str());
         health_->poison(m);
       }

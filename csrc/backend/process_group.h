@@ -578,6 +578,7 @@ class ProcessGroupMI355X : public c10d::Backend {
     bool valid;       // IPC result(s) matched the reference engine's on every rank
     std::string algo;
     int iters;        // timed runs per engine (median taken)
+    bool async_capped = false;  // key of async_op calls run at PDCC_IPC_ASYNC_GRID workgroups
   };
   std::vector<TuneRecord> autotune_table();
 
@@ -631,8 +632,11 @@ class ProcessGroupMI355X : public c10d::Backend {
   // run every candidate once via `run(k)` (on scratch buffers), check `same(0, k)` against the
   // reference, then time interleaved runs of each (median), agree across ranks (host transport),
   // remember and return the winner
+  // `ref_check` (reductions): when the reference is the IPC engine itself (no RCCL, above the host
+  // tuning range), run it and the host transport on a prefix of the caller's data and compare
   Algo autotune(const TuneKey& key, size_t bytes, DeviceState& ds, const std::vector<Algo>& cands,
-                const std::function<void(size_t)>& run, const std::function<bool(size_t, size_t)>& same);
+                const std::function<void(size_t)>& run, const std::function<bool(size_t, size_t)>& same,
+                const std::function<bool()>& ref_check = nullptr);
 
   // one engine's enqueue of each collective on stream `s` (HOST: synchronous)
   void enqueue_allreduce(Algo a, const at::Tensor& w, kern::DType kd, kern::RedOp ko, ncclDataType_t nd,

@@ -167,6 +167,7 @@ PYBIND11_MODULE(_C, m) {
                d["ipc_valid"] = r.valid;
                d["algo"] = r.algo;
                d["iters"] = r.iters;
+               d["async_capped"] = r.async_capped;
                l.append(d);
              }
              return l;

@@ -704,6 +704,24 @@ size_t IpcComm::zc_mappings() const {
   return n;
 }
 
+std::string IpcComm::describe_error(uint32_t w) {
+  if (w == 0) return "none";
+  if (w == kAbortWord) return "0x200: aborted by the host (watchdog / abort_group)";
+  const char* what = "unknown";
+  switch (w & ~0xffu) {
+    case 0x100u: what = "block-pairwise barrier"; break;
+    case 0x300u: what = "LL flag poll"; break;
+    case 0x400u: what = "zero-copy gate wait"; break;
+    case 0x800u: what = "device-side record exchange"; break;
+    case 0x900u: what = "dynamic protocol departure (done word)"; break;
+    case 0xA00u: what = "dynamic protocol ready word"; break;
+    default: break;
+  }
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "0x%x: %s timed out on rank %u", w, what, w & 0xffu);
+  return buf;
+}
+
 uint32_t IpcComm::error_word() const { return err_host_ ? __atomic_load_n(err_host_, __ATOMIC_ACQUIRE) : 0u; }
 void IpcComm::clear_error() {
   if (err_host_) __atomic_store_n(err_host_, 0u, __ATOMIC_RELEASE);

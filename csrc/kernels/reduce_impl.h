@@ -471,7 +471,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
       const uint32_t j = it - nc, cc = j / (W - 1), k = j - cc * (W - 1);
       const int q = (me + 1 + (int)((k + cc) % (W - 1))) % W;
       if (threadIdx.x == 0) {
-        s_ok = ok && dyn_wait(v, dyn_words(v, q, kern::kDynReadyOffset) + cc, dep, 0x800u) ? 1u : 0u;
+        s_ok = ok && dyn_wait(v, dyn_words(v, q, kern::kDynReadyOffset) + cc, dep, 0xA00u) ? 1u : 0u;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
         drain_vm();
       }
@@ -750,7 +750,7 @@ __device__ __forceinline__ uint2 ll_poll(const IpcView& v, uint32_t par, uint32_
     if ((uint32_t)(a >> 32) == ep && (uint32_t)(b >> 32) == ep) break;
     if ((it & 63u) == 0) {  // bounded spin; a host abort or another thread's timeout stops it too
       if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks) {
-        __hip_atomic_store(v.err, 0x200u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(v.err, 0x300u | (uint32_t)v.rank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         live = false;
       } else if (__hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
         live = false;

@@ -19,7 +19,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_ZC_ASYNC | 1 | zero-copy calls exchange their buffer records on a per-device launcher thread: the caller's host never waits for its peers (0: inline exchange) |
 | PDCC_IPC_LL_MAX | 256K | collectives up to this size per rank / chunk (max 256K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
-| PDCC_IPC_ASYNC_GRID | 64 | workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; must agree across ranks like async_op itself (0: no cap) |
+| PDCC_IPC_ASYNC_GRID | 0 | opt-in workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; with a cap set every rank must pass the same async_op to each collective (torch treats async_op as rank-local; PDCC_DEBUG=1 checks it) (0: no cap) |
 | PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
 | PDCC_IPC_DYN | 3 | chunks per workgroup of the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier), which the autotuner races for zero-copy all_reduce keys; 0: not raced; agreed group-wide (minimum) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
@@ -93,7 +93,7 @@ class Config:
     ipc_zc_cache: int = 16
     ipc_zc_async: bool = True
     ipc_zx: bool = True
-    ipc_async_grid: int = 64
+    ipc_async_grid: int = 0
     ipc_spin_ms: int = 600000
     ipc_grid: int = 512
     ipc_wide_grid: int = 1024

@@ -1781,8 +1781,9 @@ def phase_trace_probe(rank, size, device="cuda", calls=6, mib=8):
 
 def dyn_stress(rank, size, device="cuda", calls=60):
     """The dynamic zero-copy all-reduce (PDCC_ALGO=ipc_dyn) over many calls: sizes from a few
-    chunks to thousands, synchronous and async (capped grid: another chunk size), interleaved
-    with LL all_reduces and a barrier; integer-valued data so every sum is exact."""
+    chunks to thousands, synchronous and async (with PDCC_IPC_ASYNC_GRID set: the capped grid,
+    another chunk size), interleaved with LL all_reduces and a barrier. Position-dependent,
+    integer-valued data (exact in fp32): a wrong row, chunk or peer index changes the result."""
     import torch
     import torch.distributed as dist
 
@@ -1790,39 +1791,96 @@ def dyn_stress(rank, size, device="cuda", calls=60):
 
     d = _dev(device)
     b = be.native_backend(None, "cuda")
+    W = size
+    tri = W * (W + 1) / 2
+
+    def pos(n):  # 0..1020 by position (no period aligned to a tile or chunk)
+        return (torch.arange(n, device=d) % 1021).float()
+
     sizes = [(1 << 20) // 4, (8 << 20) // 4 + 3, (64 << 20) // 4, (3 << 20) // 4 + 1024]
     bufs = [torch.empty(n, device=d) for n in sizes]
+    bases = [pos(n) for n in sizes]
     small = torch.empty(1000, device=d)
-    ag_in = torch.empty((4 << 20) // 4, device=d)
-    ag_out = torch.empty(size * ag_in.numel(), device=d)
-    rs_in = torch.empty(size * ((4 << 20) // 4), device=d)
-    rs_out = torch.empty((4 << 20) // 4, device=d)
+    m = (4 << 20) // 4
+    ag_in = torch.empty(m, device=d)
+    ag_out = torch.empty(size * m, device=d)
+    rs_in = torch.empty(size * m, device=d)
+    rs_out = torch.empty(m, device=d)
+    base_m, base_rs = pos(m), pos(size * m)
     ok, engines = True, set()
     for i in range(calls):
-        x = bufs[i % len(bufs)]
-        x.fill_(float(rank + 1 + i % 7))
+        k = i % len(bufs)
+        x, base = bufs[k], bases[k]
+        torch.add(base * (rank + 1), float(i % 7), out=x)
         if i % 3 == 2:
             dist.all_reduce(x, async_op=True).wait()
         else:
             dist.all_reduce(x)
         engines.add(b.last_algo())
-        want = float(sum(r + 1 + i % 7 for r in range(size)))
-        ok = ok and bool(torch.all(x == want))
+        ok = ok and bool(torch.equal(x, base * tri + W * (i % 7)))
         if i % 5 == 4:
             small.fill_(1.0)
             dist.all_reduce(small)
             ok = ok and bool(torch.all(small == size))
         if i % 4 == 1:  # the dynamic all-gather and reduce-scatter (4 MiB per rank)
-            ag_in.fill_(float(rank + i))
+            torch.add(base_m, float(1000 * rank + i), out=ag_in)
             dist.all_gather_into_tensor(ag_out, ag_in)
             engines.add(b.last_algo())
-            want_ag = torch.arange(size, device=d, dtype=torch.float32).repeat_interleave(ag_in.numel()) + i
+            want_ag = torch.cat([base_m + float(1000 * r + i) for r in range(size)])
             ok = ok and bool(torch.equal(ag_out, want_ag))
-            rs_in.fill_(float(rank + 1 + i % 3))
+            torch.add(base_rs * (rank + 1), float(i % 3), out=rs_in)
             dist.reduce_scatter_tensor(rs_out, rs_in)
             engines.add(b.last_algo())
-            ok = ok and bool(torch.all(rs_out == float(sum(r + 1 + i % 3 for r in range(size)))))
+            want_rs = base_rs[rank * m:(rank + 1) * m] * tri + W * (i % 3)
+            ok = ok and bool(torch.equal(rs_out, want_rs))
         if i % 11 == 10:
             dist.barrier()
     torch.cuda.synchronize()
     return {"ok": ok, "engines": sorted(engines), "desc": b.describe()}
+
+
+def mixed_async_op(rank, size, device="cuda", expect_error=False):
+    """Rank 0 issues every all_reduce / all_gather / reduce_scatter with async_op=True, the other
+    ranks synchronously (torch treats async_op as rank-local). Position-dependent data; every
+    result exact. `expect_error`: return the first error instead (PDCC_DEBUG with a cap set)."""
+    import re
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    tri = size * (size + 1) / 2
+    asy = rank == 0
+    ok = True
+    try:
+        for n in (1000, (256 << 10) // 4 + 5, (4 << 20) // 4 + 7, (24 << 20) // 4):
+            base = (torch.arange(n, device=d) % 1021).float()
+            for _ in range(3):
+                x = base * (rank + 1)
+                w = dist.all_reduce(x, async_op=asy)
+                if asy:
+                    w.wait()
+                ok = ok and bool(torch.equal(x, base * tri))
+            m = max(1, n // size)
+            ag_in = base[:m] + 1000.0 * rank
+            ag_out = torch.empty(size * m, device=d)
+            w = dist.all_gather_into_tensor(ag_out, ag_in, async_op=asy)
+            if asy:
+                w.wait()
+            ok = ok and bool(torch.equal(ag_out, torch.cat([base[:m] + 1000.0 * r for r in range(size)])))
+            rs_in = torch.cat([base[:m] * (rank + 1) + q for q in range(size)])
+            rs_out = torch.empty(m, device=d)
+            w = dist.reduce_scatter_tensor(rs_out, rs_in, async_op=asy)
+            if asy:
+                w.wait()
+            ok = ok and bool(torch.equal(rs_out, base[:m] * tri + size * rank))
+        torch.cuda.synchronize()
+    except RuntimeError as e:
+        if expect_error:
+            return {"error": str(e)[:400]}
+        raise
+    m = re.search(r"async_capped=(\d+)", b.describe())
+    return {"ok": ok, "capped": int(m.group(1)) if m else 0, "error": ""}

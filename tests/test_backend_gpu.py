@@ -408,6 +408,14 @@ def test_conformance_pass_on_shared_gpu(world):
         assert r["all_ok"], {k: v for k, v in r["checks"].items() if not v["ok"]}
         assert r["info"]["ipc_ok"] and r["info"]["ll_ok"] and r["info"]["zc_ok"], r["info"]
         assert any(k.startswith("ll/all_to_all_list") for k in r["checks"]) and "zc/all_reduce_push" in r["checks"]
+        # round 5: every engine the autotuner can adopt, coalesced, async capped, raced keys
+        for want in ("dyn/all_gather", "dyn/reduce_scatter", "staged/all_reduce", "staged/broadcast",
+                     "wide/all_reduce", "coalesced/ipc/all_reduce_x64", "coalesced/ipc/all_gather_x64",
+                     "coalesced/ipc/reduce_scatter_x64", "async_capped/ipc/all_reduce",
+                     "async_capped/ipc_dyn/all_reduce", "raced/all_reduce/float32/SUM/24MiB",
+                     "raced/all_reduce/int32/BXOR/24MiB"):
+            assert want in r["checks"], (want, sorted(r["checks"]))
+        assert not r["skipped"], r["skipped"]
 
 
 def test_zero_copy_exchange_does_not_block_the_host():
@@ -485,11 +493,13 @@ def test_random_numerics_every_protocol(mode, world):
             assert all(e.startswith(want) for e in engines), engines
 
 
+@pytest.mark.parametrize("async_grid", ["0", "64"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_dynamic_allreduce_many_calls(world):
+def test_dynamic_allreduce_many_calls(world, async_grid):
     # the dynamic protocol's per-rank epoch, claim and exit counters over 60 calls of four sizes,
-    # sync and async (capped grid), between LL all_reduces and barriers: every sum exact
-    env = {"PDCC_ALGO": "ipc_dyn", "PDCC_IPC_1SHOT_MAX": "64K"}
+    # sync and async (with the opt-in async cap: another grid, so another chunk size), between
+    # LL all_reduces and barriers; position-dependent data, every sum exact
+    env = {"PDCC_ALGO": "ipc_dyn", "PDCC_IPC_1SHOT_MAX": "64K", "PDCC_IPC_ASYNC_GRID": async_grid}
     for r in _gpu_launch(W.dyn_stress, world, env=env, timeout_s=120):
         assert r["ok"], r
         assert {"ipc_2shot_dyn_zc", "ipc_dyn_zc"} <= set(r["engines"]), r["engines"]  # all_reduce; all_gather / reduce_scatter
@@ -601,10 +611,12 @@ def test_phase_trace_records_every_block():
         assert r["slowest_exit_after_block0_us"] is not None and r["slowest_exit_after_block0_us"] < 1e5, r
 
 
-def test_async_collectives_take_the_capped_grid():
+@pytest.mark.parametrize("stream", ["auto", "comm"])
+def test_async_collectives_take_the_capped_grid(stream):
     # verdict r3 Next #4: PDCC_IPC_ASYNC_GRID caps the IPC / LL launches of async_op=True
-    # collectives (overlapped with compute); synchronous ones keep the full grid
-    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ASYNC_GRID": "16"}
+    # collectives (overlapped with compute); synchronous ones keep the full grid -- also with
+    # PDCC_STREAM=comm, where they run on the comm stream too
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ASYNC_GRID": "16", "PDCC_STREAM": stream}
     for r in _gpu_launch(W.async_grid_probe, 2, env=env, timeout_s=120):
         assert r["ok"], r
         for k, v in r.items():
@@ -612,3 +624,21 @@ def test_async_collectives_take_the_capped_grid():
                 assert v == 0, r
             elif k.startswith("async_capped"):
                 assert v >= 6, r
+
+
+@pytest.mark.parametrize("algo", ["ipc", "ipc_dyn", "auto"])
+def test_ranks_mixing_async_op_are_correct(algo):
+    # torch treats async_op as rank-local. With the async grid cap off (the
+    # default) rank 0 issuing async_op=True while rank 1 issues the same collective synchronously
+    # must be exact on every protocol size (LL, 1-shot, zero-copy 2-shot + staged rest)
+    for r in _gpu_launch(W.mixed_async_op, 2, env={"PDCC_ALGO": algo}, timeout_s=120):
+        assert r["ok"], r
+        assert r["capped"] == 0, r
+
+
+def test_mixed_async_op_with_cap_is_caught_by_debug():
+    # with the opt-in cap set, mixing async_op would pair different grids: PDCC_DEBUG=1's
+    # fingerprint check turns that into an error on every rank before anything launches
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ASYNC_GRID": "16", "PDCC_DEBUG": "1"}
+    for r in _gpu_launch(W.mixed_async_op, 2, args=("cuda", True), env=env, timeout_s=120):
+        assert "async_op differs" in r["error"], r
