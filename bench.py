@@ -187,6 +187,16 @@ def run_rank(args):
     ngpu = torch.cuda.device_count() if on_gpu else 0
     with section("rccl_env_sweep"):
         EXTRAS_PARTIAL["rccl_env_sweep"] = rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args)
+    if on_gpu and ngpu < world:
+        # ranks sharing a GPU (functional rehearsals only): each process's streams take their own
+        # hardware queues, and past the number the GPU maps at once the hardware time-slices them
+        # -- a rank's IPC kernel then waits a scheduling quantum for its peer (W = 8 after the
+        # conformance pass: 56 ms per op at unchanged kernel bodies, scripts/queue_slicing_probe.py,
+        # profiles/r5/). GPU_MAX_HW_QUEUES=1 per rank (set before the ranks start) avoids it; the
+        # record says which it was.
+        q = os.environ.get("GPU_MAX_HW_QUEUES", "")
+        EXTRAS_PARTIAL["shared_gpu"] = {"ranks": world, "gpus": ngpu, "gpu_max_hw_queues": q or "default",
+                                        "may_time_slice": q != "1"}
     if on_gpu:
         local = local % ngpu  # (ranks > GPUs only in functional rehearsals on a 1-GPU box)
         torch.cuda.set_device(local)

@@ -127,6 +127,9 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
     const size_t sig = granule(kern::ipc_signal_bytes());
     my_flags_ = static_cast<uint32_t*>(alloc_exportable(sig, true, mine));
     PDCC_HIP(hipMemset(my_flags_, 0, sig));
+    // the dynamic protocols' own control words: ordinary device memory (only this device's blocks)
+    PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&dyn_ctl_), kern::kDynCtlBytes));
+    PDCC_HIP(hipMemset(dyn_ctl_, 0, kern::kDynCtlBytes));
     if (const char* ep = std::getenv("PDCC_TEST_ZX_EPOCH")) {  // test hook: start the exchange epoch near the wrap
       const uint32_t v = (uint32_t)std::strtoul(ep, nullptr, 0);
       PDCC_HIP(hipMemcpy(reinterpret_cast<char*>(my_flags_) + kern::kZxEpochOffset, &v, sizeof(v),
@@ -199,6 +202,7 @@ IpcComm::~IpcComm() {
     for (void* m : flags_maps_)
       if (m) hipIpcCloseMemHandle(m);
     if (my_flags_) hipFree(my_flags_);
+    if (dyn_ctl_) hipFree(dyn_ctl_);
     if (err_host_) hipHostFree(err_host_);
     gate_last_.clear();
     if (gates_host_) hipHostFree(gates_host_);
@@ -315,6 +319,7 @@ kern::IpcView IpcComm::view(const std::vector<char*>& bufs) const {
   }
   v.err = err_dev_;
   v.counters = my_flags_ + kern::kCountWord;
+  v.dctl = dyn_ctl_;
   v.cap = cap_;
   v.rank = rank_;
   v.world = world_;

@@ -290,6 +290,7 @@ class IpcComm {
   uint64_t async_capped_ = 0;  // launches the async cap applied to
 
   uint32_t* my_flags_ = nullptr;          // uncached device memory
+  uint32_t* dyn_ctl_ = nullptr;           // the dynamic protocols' control words (kern::IpcView::dctl)
   std::vector<uint32_t*> peer_flags_;     // mapped (own entry = my_flags_)
   std::vector<void*> flags_maps_;         // hipIpcOpenMemHandle results to close (may precede the pointer)
   uint32_t* err_host_ = nullptr;          // pinned, device-visible

@@ -32,6 +32,10 @@ ncclConfig_t make_config(const RcclOpts& o, bool for_split) {
   cfg.blocking = o.nonblocking ? 0 : 1;  // non-blocking: creation is polled against a deadline (wait_ready)
   if (o.min_ctas > 0) cfg.minCTAs = o.min_ctas;
   if (o.max_ctas > 0) cfg.maxCTAs = o.max_ctas;
+  // RCCL validates the pair as given: a floor with the ceiling left undefined is rejected
+  // ("Invalid config min/max channels attribute value 28/-2147483648", found by the world-1 RCCL
+  // rehearsal of bench.py's CTA sweep): a floor alone means exactly that many channels
+  if (o.min_ctas > 0 && cfg.maxCTAs < o.min_ctas) cfg.maxCTAs = o.min_ctas;
   if (for_split) cfg.splitShare = o.split_share ? 1 : 0;
   return cfg;
 }

@@ -68,17 +68,17 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 // input (owners rotated per item) into out[q]; the claim loop and departure of the dynamic
 // all-reduce (reduce_impl.h).
 template <int W>
-__device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c, char* lds) {
+__device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c, char* lds, const PhaseTrace* tr) {
   const size_t nt = c.bytes / kTile;
   const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
-  const uint32_t dep = dyn_epoch(v);
-  dyn_claim_loop(v, nc, [&](uint32_t it) {
+  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
+  dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(v.rank + it), t0, 1, t1};
     ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
   });
-  dyn_depart(v, dep, true);
+  dyn_depart(v, dep, true, c.test_flags, tr);
 }
 
 // Zero-copy copies (IpcCall::zc): peers' user buffers are read in place; data
@@ -93,7 +93,7 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
   tr.mark(2);
   tr.mark(4);
   if (c.coll == IpcColl::ALLGATHER && c.dyn) {
-    ipc_allgather_dyn<W>(v, c, lds);
+    ipc_allgather_dyn<W>(v, c, lds, &tr);
     tr.mark(5);
     return;
   }

@@ -463,6 +463,14 @@ struct PhaseTrace {
   __device__ __forceinline__ void mark(int k) const {
     if (on) slots()[k] = __builtin_amdgcn_s_memrealtime();
   }
+  // accumulating words (the dynamic protocols' totals): now() -> ... -> add(k, t0)
+  __device__ __forceinline__ uint64_t now() const { return on ? __builtin_amdgcn_s_memrealtime() : 0; }
+  __device__ __forceinline__ void add(int k, uint64_t t0) const {
+    if (on) slots()[k] += __builtin_amdgcn_s_memrealtime() - t0;
+  }
+  __device__ __forceinline__ void count(int k, uint64_t n = 1) const {
+    if (on) slots()[k] += n;
+  }
   __device__ __forceinline__ void finish(const kern::IpcView& view) const {
     if (!on) return;
     uint64_t* t = slots();

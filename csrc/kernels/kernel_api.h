@@ -120,6 +120,11 @@ struct IpcViewT {
   P<uint64_t> trace;             // PDCC_IPC_TRACE: ring of kTraceWords-word records (host-mapped), or null
   uint32_t trace_cap;            // records in the ring
   uint32_t trace_slot;           // this launch's record (the host's launch counter % trace_cap)
+  // this rank's control words of the dynamic protocols (claim / exit counters, epoch: word
+  // indices kDynClaimWord / kDynExitWord / kDynEpochWord) in ordinary device memory -- only
+  // this device's blocks touch them (agent-scope atomics), and an atomic on the uncached
+  // signal area serialises at the memory controller
+  P<uint32_t> dctl;
 };
 using IpcView = IpcViewT<RawPtr>;
 
@@ -130,8 +135,12 @@ using IpcView = IpcViewT<RawPtr>;
 // [8] every rank's record in, [9] mapping lookup done, [10] every vote in, [11] verdict published.
 // [12] after the block's call number was taken, and inside the zero-copy arrival barrier: [13] every
 // wave drained (before the release), [14] flags stored to the peers, [15] every peer's flag seen.
+// Dynamic protocols (block 0's totals, ticks): [16] waiting for claimed items, [17] publishing
+// ready words (drain + release + store), [18] waiting for peers' ready words (+ acquire),
+// [19] departure (exit count, and for the last block the done exchange), [20] items run,
+// [21] of them phase-1 items, [22] 1 = block 0 departed last, [23] reading the call's epoch.
 // Record `trace_slot` (one per launch, whatever the grid).
-constexpr int kTraceWords = 16;
+constexpr int kTraceWords = 24;
 // After the header, per block b < kTraceBlocks: [kTraceWords + b] the block's first pull /
 // reduce done ([5]), [kTraceWords + kTraceBlocks + b] its exit ([7]) -- how far the slowest
 // block trails block 0.
@@ -234,6 +243,7 @@ constexpr size_t kZxBytes = 1024 + kGateSlots * sizeof(GateSlot);
 // ready word per chunk. Words hold a per-rank dyn-call epoch (never 0), compared for equality.
 constexpr size_t kDynOffset = kZxOffset + kZxBytes;
 // (u32 word indices from kDynOffset; the two counters every block hits sit 128 B apart)
+constexpr size_t kDynCtlBytes = 512;  // IpcView::dctl (and the round-4 copy at kDynOffset)
 constexpr int kDynEpochWord = 0;   // epoch of this rank's last finished dyn call
 constexpr int kDynClaimWord = 32;  // work-item counter of the running call (reset by its last block)
 constexpr int kDynExitWord = 64;   // blocks of the running call that finished (reset by the last one)
@@ -284,7 +294,9 @@ struct IpcCallT {
   int dyn;  // > 0: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol with about `dyn` chunks per
             // workgroup (see kDynOffset); staged runs ignore it
   int test_flags;  // PDCC_TEST_IPC_FLAGS, measurements only: bit 0 = the zero-copy reductions' arrival
-                   // barrier without its release / acquire (what the data hand-over costs)
+                   // barrier without its release / acquire (what the data hand-over costs); bits 1-2:
+                   // reduce_impl.h zc pipes; bit 3 = dyn claims from the first item (round-4 claim
+                   // loop); bit 4 = dyn control words in the uncached signal area (round-4 placement)
 };
 using IpcCall = IpcCallT<RawPtr>;
 

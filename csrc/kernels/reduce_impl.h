@@ -386,36 +386,59 @@ __device__ __forceinline__ bool dyn_wait(const DView& v, const uint32_t* w, uint
 // positions I write in phase 2 (tile q + W*r of MY tensor) were read by q in its phase 1 of
 // chunk c, which q finished before publishing ready[c]; my own tiles are written in phase 1
 // only, and peers read them after my ready word.
+// This rank's control words (claim / exit counters, epoch): ordinary device memory (IpcView::dctl),
+// or -- PDCC_TEST_IPC_FLAGS bit 4, A/B only -- the round-4 copy in the uncached signal area.
+__device__ __forceinline__ uint32_t* dyn_ctl(const DView& v, int flags) {
+  return (flags & 16) ? dyn_words(v, v.rank, kern::kDynOffset) : (uint32_t*)v.dctl;
+}
+
 // This call's epoch: the previous dyn call's last block stored its own (never 0).
-__device__ __forceinline__ uint32_t dyn_epoch(const DView& v) {
+__device__ __forceinline__ uint32_t dyn_epoch(const DView& v, int flags, const PhaseTrace* tr) {
   __shared__ uint32_t s_dep;
   if (threadIdx.x == 0) {
-    const uint32_t e = __hip_atomic_load(dyn_words(v, v.rank, kern::kDynOffset) + kern::kDynEpochWord,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    const uint64_t t0 = tr->now();
+    const uint32_t e =
+        __hip_atomic_load(dyn_ctl(v, flags) + kern::kDynEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_dep = e ? e : 1u;
+    tr->add(23, t0);
   }
   __syncthreads();
   return s_dep;
 }
 
-// Claim loop: item(it) for every item this block claims, it < total. Block b's first item is item
-// b (no counter traffic at launch: every block hitting one uncached word at once serialises at the
-// memory controller -- a fixed ~17 us at any size on one MI355X); later items are G + the counter.
-// Thread 0 claims one item ahead, so the atomic's round trip overlaps the current item. Claims are
-// monotonic (b < G <= G + k): a block never holds an earlier item behind a later one.
+// Claim loop: item(it) for every item this block claims, it < total. Items [0, 2G) are static --
+// block b runs b, then b + G -- and only later items are claimed, as 2G + the counter: every block
+// hitting one word at launch serialises at the memory side (round 4 measured a fixed ~17 us per
+// call on the uncached word at any size, round 5's trace: profiles/r5/), and a call with at most 2G
+// items claims nothing at all. Thread 0 claims one item ahead (from its second item on), so the
+// atomic's round trip overlaps the current item. Claims are monotonic (b < b + G < 2G <= 2G + k): a
+// block never holds an earlier item behind a later one, and a block's earlier items are always
+// smaller, so every phase-1 item (index < nc, waiting for nothing) is reached without a wait.
+// PDCC_TEST_IPC_FLAGS bit 3 (A/B only): the round-4 loop (item b, then G + the counter, claimed
+// from the first item on).
 template <class Item>
-__device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, Item&& item) {
+__device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, int flags, const PhaseTrace* tr,
+                                               Item&& item) {
   __shared__ uint32_t s_item;
-  uint32_t* const claim = dyn_words(v, v.rank, kern::kDynOffset) + kern::kDynClaimWord;
+  uint32_t* const claim = dyn_ctl(v, flags) + kern::kDynClaimWord;
+  const uint32_t G = gridDim.x;
+  const bool old = (flags & 8) != 0;
+  const uint32_t base = old ? G : 2u * G;  // first claimed item
   uint32_t next = blockIdx.x;
   for (;;) {
-    if (threadIdx.x == 0) s_item = next;
+    const uint64_t t0 = tr->now();
+    if (threadIdx.x == 0) s_item = next;  // (waits for the claim's return)
     __syncthreads();
     const uint32_t it = s_item;
     __syncthreads();  // (s_item is rewritten by the next claim)
+    if (threadIdx.x == 0) tr->add(16, t0);
     if (it >= total) break;
-    if (threadIdx.x == 0)
-      next = gridDim.x + __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      if (!old && it < G) next = it + G;  // the second static item
+      else next = total > base ? base + __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : total;
+      tr->count(20);
+    }
     item(it);
   }
 }
@@ -423,9 +446,10 @@ __device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, I
 // Departure: once every block of mine is done (exit counter), the last one tells every peer, waits
 // until every peer's blocks are done too (nobody reads my tensor any more), then resets the counters
 // and publishes this call's epoch for the next dyn call.
-__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok) {
+__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok, int flags, const PhaseTrace* tr) {
   const int me = v.rank, W = v.world;
-  uint32_t* const ctl = dyn_words(v, me, kern::kDynOffset);
+  uint32_t* const ctl = dyn_ctl(v, flags);
+  const uint64_t t0 = tr->now();
   drain_vm();
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -440,12 +464,14 @@ __device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok
       __hip_atomic_store(ctl + kern::kDynClaimWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl + kern::kDynExitWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctl + kern::kDynEpochWord, dep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      tr->count(22);
     }
+    tr->add(19, t0);
   }
 }
 
 template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds) {
+__device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds, const PhaseTrace* tr) {
   constexpr int D = DepthFor<W>::value;
   const int me = v.rank;
   const size_t nrows = c.bytes / kTile / W;
@@ -453,27 +479,32 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
   const uint32_t nc = (uint32_t)((nrows + K - 1) / K);
   uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
   __shared__ uint32_t s_ok;
-  const uint32_t dep = dyn_epoch(v);
+  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
   bool ok = true;
-  dyn_claim_loop(v, nc * W, [&](uint32_t it) {
+  dyn_claim_loop(v, nc * W, c.test_flags, tr, [&](uint32_t it) {
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
       zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div, c.test_flags);
+      const uint64_t t0 = tr->now();
       drain_vm();  // every wave's stores and loads (a peer overwrites what I read once it sees ready)
       __syncthreads();
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: write back L2 dirty lines
         drain_vm();
         __hip_atomic_store(ready + it, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        tr->add(17, t0);
+        tr->count(21);
       }
     } else {
       const uint32_t j = it - nc, cc = j / (W - 1), k = j - cc * (W - 1);
       const int q = (me + 1 + (int)((k + cc) % (W - 1))) % W;
       if (threadIdx.x == 0) {
+        const uint64_t t0 = tr->now();
         s_ok = ok && dyn_wait(v, dyn_words(v, q, kern::kDynReadyOffset) + cc, dep, 0xA00u) ? 1u : 0u;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: drop stale L1/L2 lines
         drain_vm();
+        tr->add(18, t0);
       }
       __syncthreads();
       ok = s_ok != 0;
@@ -485,25 +516,26 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
       }
     }
   });
-  dyn_depart(v, dep, ok);
+  dyn_depart(v, dep, ok, c.test_flags, tr);
 }
 
 // Dynamic zero-copy reduce-scatter (IpcCall::dyn): my output chunk in items of K tiles, each reduced
 // from every rank's flat input (chunk `me` at me * zstride) -- one phase, no ready words; the
 // departure keeps every peer's input alive until the last reader is done.
 template <DType DT, RedOp OP, int W>
-__device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCall& c, char* lds) {
+__device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCall& c, char* lds,
+                                                       const PhaseTrace* tr) {
   constexpr int D = DepthFor<W>::value;
   const size_t nt = c.bytes / kTile;
   const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
-  const uint32_t dep = dyn_epoch(v);
-  dyn_claim_loop(v, nc, [&](uint32_t it) {
+  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
+  dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const AllSrcMap<W> m{&v, (size_t)v.rank * c.zstride, (char*)c.out[0], c.bytes, t0, 1, t1};
     ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
   });
-  dyn_depart(v, dep, true);
+  dyn_depart(v, dep, true, c.test_flags, tr);
 }
 
 // Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
@@ -524,12 +556,12 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   tr.mark(2);
   tr.mark(4);
   if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
-    ipc_allreduce_dyn<DT, OP, W>(v, c, lds);
+    ipc_allreduce_dyn<DT, OP, W>(v, c, lds, &tr);
     tr.mark(5);
     return;
   }
   if (c.coll == IpcColl::REDUCE_SCATTER && c.dyn) {
-    ipc_reduce_scatter_dyn<DT, OP, W>(v, c, lds);
+    ipc_reduce_scatter_dyn<DT, OP, W>(v, c, lds, &tr);
     tr.mark(5);
     return;
   }

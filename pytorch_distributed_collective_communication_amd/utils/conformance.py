@@ -354,18 +354,19 @@ def run(rank: int, world: int, dev, deadline_s: float = 45.0, max_bytes: int = 6
                 dist.all_reduce(t, group=g)
                 return _close(t, xs, "SUM", W, "float32")
 
+            # (per-rank payloads of 4 MiB at every W: the zero-copy threshold, PDCC_IPC_ZC_MIN = 1 MiB,
+            # applies to one rank's input / output chunk -- 4 MiB / W would run staged from W = 5 on)
             def zc_all_gather():
-                xs = [_seeded((n // W,), f32, 1400 + r, dev) for r in range(W)]
-                out = torch.empty(n // W * W, device=dev)
+                xs = [_seeded((n,), f32, 1400 + r, dev) for r in range(W)]
+                out = torch.empty(n * W, device=dev)
                 dist.all_gather_into_tensor(out, xs[rank], group=g)
                 return bool(torch.equal(out, torch.cat(xs)))
 
             def zc_reduce_scatter():
-                xs = [_seeded((n,), f32, 1500 + r, dev) for r in range(W)]
-                m = n // W
-                out = torch.empty(m, device=dev)
+                xs = [_seeded((n * W,), f32, 1500 + r, dev) for r in range(W)]
+                out = torch.empty(n, device=dev)
                 dist.reduce_scatter_tensor(out, xs[rank], group=g)
-                return _close(out, [x[rank * m:(rank + 1) * m] for x in xs], "SUM", W, "float32")
+                return _close(out, [x[rank * n:(rank + 1) * n] for x in xs], "SUM", W, "float32")
 
             def zc_broadcast():
                 src = _seeded((n,), f32, 1600, dev)

@@ -5,7 +5,10 @@ of the 2-shot all_reduce (zero-copy and staged) with W ranks sharing ONE GPU, ne
 
 PDCC_IPC_TRACE records block 0's s_memrealtime stamps (100 MHz) per launch
 (kern::kTraceWords): [1] entry, [2] arrival barrier, [3] gate passed / staged,
-[4] data barrier, [5] phase 1 (reduce own tiles) done, [6] second barrier, [7] exit.
+[4] data barrier, [5] phase 1 (reduce own tiles) done, [6] second barrier, [7] exit;
+the dynamic protocols add block 0's totals: [16] claim waits, [17] ready publishing,
+[18] ready waits, [19] departure, [20] items, [21] phase-1 items, [22] departed last,
+[23] epoch read.
 Per phase the median over the timed calls, in microseconds, plus the HBM traffic
 model of each protocol and the rates it implies:
 
@@ -68,6 +71,15 @@ def work(rank, size, mib, iters):
               # inside: call number taken, every wave drained, flags stored, every peer's flag seen
               "block_seq": ph(3, 12), "barrier_drain": ph(12, 13), "barrier_store": ph(13, 14),
               "barrier_poll": ph(14, 15), "barrier_acquire": ph(15, 2)}
+    # dynamic protocols (--algo ipc_dyn): block 0's totals per call (words 16-23)
+
+    def tot(k, scale=100.0):
+        v = [r[k] / scale for r in recs if len(r) > 23]
+        return round(statistics.median(v), 1) if v and any(v) else None
+
+    phases.update({"dyn_claim_wait": tot(16), "dyn_ready_publish": tot(17), "dyn_ready_wait": tot(18),
+                   "dyn_departure": tot(19), "dyn_items_block0": tot(20, 1.0), "dyn_phase1_items_block0": tot(21, 1.0),
+                   "dyn_block0_last": tot(22, 1.0), "dyn_epoch_read": tot(23)})
     out = {"rank": rank, "engine": b.last_algo(), "correct": ok, "wall_us": round(statistics.median(walls) * 1e6, 1),
            "phases_us": phases, "records": len(recs), "blocks_us": block_spread(recs)}
     # K1 at the same total workgroup budget: rank 0 alone, the others wait
@@ -91,7 +103,7 @@ def work(rank, size, mib, iters):
     return out
 
 
-HDR, NB = 16, 256  # kern::kTraceWords, kern::kTraceBlocks
+HDR, NB = 24, 256  # kern::kTraceWords, kern::kTraceBlocks
 
 
 def block_spread(recs):

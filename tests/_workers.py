@@ -1764,7 +1764,7 @@ def phase_trace_probe(rank, size, device="cuda", calls=6, mib=8):
         dist.all_reduce(x)
         ok = ok and bool(torch.all(x == size * (size + 1) / 2))
     torch.cuda.synchronize()
-    HDR, NB = 16, 256
+    HDR, NB = 24, 256  # kern::kTraceWords, kern::kTraceBlocks
     recs = [r for r in b.ipc_trace() if r[1] and r[7]]
     out = {"ok": ok, "engine": b.last_algo(), "records": len(recs), "rec_words": len(recs[-1]) if recs else 0}
     if recs:
