@@ -810,6 +810,7 @@ def baseline_configs(world, rank, dev, x, group=None, engine=None):
             rec(f"all_reduce_{size_label(n2 * 4)}_w2", "all_reduce", n2 * 4,
                 lambda: dist.all_reduce(x[:n2], group=g))
         per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
+        per = min(per, _shared_gpu_cap(world, dev) // 2)
         ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)
         ag_out = torch.empty(per * world, dtype=torch.bfloat16, device=dev)
         rec(f"all_gather_bf16_{size_label(per * 2)}_per_rank", "all_gather", per * 2 * world,
@@ -841,6 +842,22 @@ def torch_nccl_compare(world, rank, dev, native, x):
     finally:
         dist.destroy_process_group(g)
     return {"rows": rows}
+
+
+def _shared_gpu_cap(world, dev) -> int:
+    """Per-rank input bytes of the ZeRO-style all-gather row that fit when ranks share a GPU (rehearsals:
+    W ranks x (input + W x input) on one device -- 8 x 36 GiB at full size would not fit 288 GB). The
+    same value on every rank (device total, world and device count only): a power of two, at most
+    40 % of the device per GPU's worth of ranks. One rank per GPU: no cap."""
+    import torch
+
+    ngpu = torch.cuda.device_count()
+    if ngpu >= world:
+        return 1 << 62
+    per_gpu = -(-world // ngpu)
+    total = torch.cuda.get_device_properties(dev).total_memory
+    cap = max(1 << 20, int(0.4 * total / (per_gpu * (world + 1))))
+    return 1 << (cap.bit_length() - 1)  # a power of two: the row's name stays a round size
 
 
 def size_label(nbytes: int) -> str:

@@ -64,7 +64,7 @@ Algo ProcessGroupMI355X::tuned(const TuneKey& k) {
 // (topology, dtype/op support, the consensus table), so every rank picks the same.
 Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceState& ds, Algo a0, bool rccl_can,
                                 bool ipc_can, const std::function<Algo(const TuneKey&, const std::vector<Algo>&)>& tune) {
-  const auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok, ds.ll_ok);
+  auto cands = tune_candidates(c, bytes, rccl_can, ipc_can, ds.zc_ok, ds.ll_ok);
   if (cands.empty()) return a0;
   // an async call whose IPC launches run the capped grid (PDCC_IPC_ASYNC_GRID) is a key of its own
   // (bucket + kAsyncBucket): a verdict timed at one grid is never applied at the other
@@ -94,8 +94,28 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
   // every engine of the race exists before the clock starts (communicator setup is not timed)
   for (Algo a : cands) {
     if (a == Algo::RCCL) rccl(ds);
-    if (a == Algo::RCCL_WIDE) rccl_wide(ds);
     if (is_ipc(a)) ipc(ds);
+  }
+  if (std::find(cands.begin(), cands.end(), Algo::RCCL_WIDE) != cands.end()) {
+    // an optional candidate: a wide child communicator this RCCL build refuses (a channel count it
+    // does not take) leaves the race on every rank -- and the group's later keys -- instead of
+    // poisoning the group the headline runs on
+    double ok = 1.0;
+    std::string why;
+    try {
+      rccl_wide(ds, /*fatal=*/false);
+    } catch (const std::exception& e) {
+      ok = 0.0;
+      why = e.what();
+    }
+    shm().allreduce(&ok, 1, at::kDouble, RedOpType::MIN, timeout_);
+    if (ok <= 0.0) {
+      fprintf(stderr, "[pdcc r%d] wide RCCL communicator (%d CTAs) unavailable, dropped from the autotuner: %s\n",
+              rank_, cfg_.rccl_wide_ctas, why.empty() ? "failed on another rank" : why.c_str());
+      cfg_.rccl_wide_ctas = 0;  // (every rank: agreed above)
+      cands.erase(std::remove(cands.begin(), cands.end(), Algo::RCCL_WIDE), cands.end());
+      if (cands.size() < 2) return a0;
+    }
   }
   // the race runs on the caller's stream: it must not overlap an async collective of this
   // group still in flight on the comm stream (IPC kernels of one rank share the per-block

@@ -85,6 +85,7 @@ Config Config::from_env() {
   c.ipc_zc = env_bool("PDCC_IPC_ZC", c.ipc_zc);
   c.ipc_push = env_bool("PDCC_IPC_PUSH", c.ipc_push);
   c.ipc_dyn = std::min(64, std::max(0, env_int("PDCC_IPC_DYN", c.ipc_dyn)));
+  c.ipc_dyn_min_rows = std::min(4096, std::max(0, env_int("PDCC_IPC_DYN_MIN_ROWS", c.ipc_dyn_min_rows)));
   c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
   c.ipc_ll_max = env_size("PDCC_IPC_LL_MAX", c.ipc_ll_max);
   c.ipc_zc_cache = std::max<size_t>(1, env_size("PDCC_IPC_ZC_CACHE", c.ipc_zc_cache));
@@ -181,7 +182,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_dyn_min_rows=" << ipc_dyn_min_rows << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms << " rccl_nonblocking=" << rccl_nonblocking
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")

@@ -47,6 +47,9 @@ struct Config {
   // PDCC_IPC_DYN: chunks per workgroup of the dynamic 2-shot all-reduce (IPC_DYN; fewer = less
   // per-item overhead, more = finer load balance); 0: the autotuner does not race it (0..64)
   int ipc_dyn = 3;
+  // PDCC_IPC_DYN_MIN_ROWS: rows (W tiles each) per dynamic item, at least (0 = kern::kDynMinRows = 16;
+  // 1..4096; voted group-wide like PDCC_IPC_DYN)
+  int ipc_dyn_min_rows = 0;
   size_t ipc_zc_min = 1u << 20;            // PDCC_IPC_ZC_MIN
   // All-reduces up to this size (<= 256 KiB, kern::kLLMaxBytes) use the LL protocol: every
   // rank pushes flag-tagged 8-byte words into its peers' signal areas and polls its own --

@@ -337,6 +337,7 @@ void ProcessGroupMI355X::enqueue_allreduce(Algo a, const at::Tensor& w, kern::DT
     if (a == Algo::IPC_WIDE) c.grid_cap = cfg_.ipc_wide_grid;  // (shared devices: capped in launch_view)
     if (a == Algo::IPC_DYN && c.coll == kern::IpcColl::ALLREDUCE_2SHOT)  // (zero-copy runs only)
       c.dyn = std::max(1, cfg_.ipc_dyn);  // chunks per workgroup
+    c.dyn_min_rows = cfg_.ipc_dyn_min_rows;
     // small (all-)reduce: flag-tagged pushes, no staging copy, no barrier
     if (ds.ll_ok && bytes_in_ll_range(w.nbytes()))
       c.coll = rooted ? kern::IpcColl::REDUCE_LL : kern::IpcColl::ALLREDUCE_LL;
@@ -427,6 +428,7 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
       return;
     }
     if (a == Algo::IPC_DYN && !rooted) c.dyn = std::max(1, cfg_.ipc_dyn);  // (zero-copy runs only)
+    c.dyn_min_rows = cfg_.ipc_dyn_min_rows;
     ipc_run(ds, c, wi.data_ptr(), bytes, kern::kTileBytes, ic.chunk_cap(), s);
   } else if (a == Algo::RCCL) {
     RcclComm& rc = rccl(ds);
@@ -546,6 +548,7 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
       return;
     }
     if (a == Algo::IPC_DYN) c.dyn = std::max(1, cfg_.ipc_dyn);  // (zero-copy runs only)
+    c.dyn_min_rows = cfg_.ipc_dyn_min_rows;
     // a flat input (reduce_scatter_tensor) is read in place by every peer
     ipc_run(ds, c, is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr, bytes * size_, kern::kTileBytes,
             ic.chunk_cap() / size_, s);

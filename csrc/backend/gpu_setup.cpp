@@ -128,24 +128,26 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
   // sets the dynamic all-reduce's chunk size (every rank must number the chunks alike) and whether the
   // autotuner races it (every rank must race the same candidates).
   {
-    const int32_t mine3[4] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid, cfg_.ipc_dyn};
+    const int32_t mine3[5] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid, cfg_.ipc_dyn,
+                              cfg_.ipc_dyn_min_rows};
     const auto gv = store_allgather(store_, "pdcc/dev_grids", rank_, size_,
                                     std::vector<uint8_t>(reinterpret_cast<const uint8_t*>(mine3),
                                                          reinterpret_cast<const uint8_t*>(mine3) + sizeof(mine3)));
-    int32_t lo[4] = {mine3[0], mine3[1], mine3[2], mine3[3]};
+    int32_t lo[5] = {mine3[0], mine3[1], mine3[2], mine3[3], mine3[4]};
     for (const auto& v : gv) {
       if (v.size() != sizeof(mine3)) continue;
-      int32_t t[4];
+      int32_t t[5];
       std::memcpy(t, v.data(), sizeof(t));
-      for (int k = 0; k < 4; ++k) lo[k] = std::min(lo[k], t[k]);
+      for (int k = 0; k < 5; ++k) lo[k] = std::min(lo[k], t[k]);
     }
-    if (lo[0] != mine3[0] || lo[1] != mine3[1] || lo[2] != mine3[2] || lo[3] != mine3[3])
-      fprintf(stderr, "[pdcc r%d] IPC grid caps / PDCC_IPC_DYN differ between ranks: using the group minimum "
-              "%d/%d/%d/%d\n", rank_, lo[0], lo[1], lo[2], lo[3]);
+    if (std::memcmp(lo, mine3, sizeof(lo)) != 0)
+      fprintf(stderr, "[pdcc r%d] IPC grid caps / PDCC_IPC_DYN / _DYN_MIN_ROWS differ between ranks: using the group "
+              "minimum %d/%d/%d/%d/%d\n", rank_, lo[0], lo[1], lo[2], lo[3], lo[4]);
     cfg_.ipc_grid = std::max(1, lo[0]);
     cfg_.ipc_wide_grid = lo[1];
     cfg_.ipc_async_grid = lo[2];
     cfg_.ipc_dyn = lo[3];
+    cfg_.ipc_dyn_min_rows = lo[4];
   }
   ds.recs = recs;
   ds.shared_device = shared;
@@ -257,7 +259,7 @@ RcclComm& ProcessGroupMI355X::rccl_create(DeviceState& ds) {
 
 // The wide child of the group's communicator (collective over the group: created by
 // decide() on every rank when a key races it, or by a forced PDCC_ALGO=rccl_wide).
-RcclComm& ProcessGroupMI355X::rccl_wide(DeviceState& ds) {
+RcclComm& ProcessGroupMI355X::rccl_wide(DeviceState& ds, bool fatal) {
   if (ds.rccl_wide) return *ds.rccl_wide;
   RcclComm& base = rccl(ds);
   const auto t0 = std::chrono::steady_clock::now();
@@ -269,7 +271,7 @@ RcclComm& ProcessGroupMI355X::rccl_wide(DeviceState& ds) {
   try {
     c = std::make_shared<RcclComm>(base, rank_, o);
   } catch (const std::exception& e) {
-    health_->poison(std::string("RCCL (wide) communicator creation failed: ") + e.what());
+    if (fatal) health_->poison(std::string("RCCL (wide) communicator creation failed: ") + e.what());
     throw;
   }
   c->tag = base.tag + "#wide";

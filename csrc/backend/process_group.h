@@ -425,7 +425,8 @@ class ProcessGroupMI355X : public c10d::Backend {
   void init_topology(DeviceState& ds);
   RcclComm& rccl(DeviceState& ds);
   RcclComm& rccl_create(DeviceState& ds);  // (rccl(): a failure poisons the group)
-  RcclComm& rccl_wide(DeviceState& ds);
+  // fatal = false (the autotuner's optional candidate): a failed creation does not poison the group
+  RcclComm& rccl_wide(DeviceState& ds, bool fatal = true);
   std::shared_ptr<PairChan> pair_chan(DeviceState& ds, int peer);
   static void pair_builder(std::shared_ptr<PairChan> pc, c10::intrusive_ptr<c10d::Store> store, std::string key,
                            int prank, int dev, int pi, int64_t init_ms);

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 template <int W>
 __device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c, char* lds, const PhaseTrace* tr) {
   const size_t nt = c.bytes / kTile;
-  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn);
+  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
   const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
   dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
@@ -140,10 +140,10 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
 
 template <int W>
 __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
-                                              uint32_t seq0) {
+                                              uint32_t seq0, bool early) {
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t seq = block_seq(v, seq0);
+  const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
   if (c.coll == IpcColl::BARRIER) {  // the arrival barrier is the whole collective
@@ -230,10 +230,11 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
-  const uint32_t seq0 = block_seq_load(v);
+  const bool early = (c.test_flags & 32) == 0;  // (see k_ipc_reduce)
+  const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_copy_body<W>(sv, sc, lds, tr, seq0);
+  ipc_copy_body<W>(sv, sc, lds, tr, seq0, early);
   tr.finish(v);
   zx_publish_verdict(c);
 }

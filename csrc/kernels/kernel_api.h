@@ -250,14 +250,20 @@ constexpr int kDynExitWord = 64;   // blocks of the running call that finished (
 constexpr size_t kDynDoneOffset = kDynOffset + 384;   // u32 per source rank: its last block's epoch
 constexpr size_t kDynReadyOffset = kDynOffset + 512;  // u32 per chunk: the epoch its owner reduced it in
 constexpr uint32_t kDynMaxChunks = 16384;
-constexpr uint32_t kDynMinRows = 8;  // rows (W tiles each) per chunk, at least
+// rows (W tiles each) per chunk, at least (IpcCall::dyn_min_rows, PDCC_IPC_DYN_MIN_ROWS; 0 = this):
+// every item is its own short pipeline (fill, drain, ready fence), so small items turn the dynamic
+// protocol latency-bound -- 16 MiB at W = 2 on one GPU: 8-row items moved the data at half the static
+// protocol's rate (profiles/r5/)
+constexpr uint32_t kDynMinRows = 16;
 constexpr size_t kDynBytes = 512 + (size_t)kDynMaxChunks * 4;
 // rows per chunk of a dyn call: about `per` chunks per workgroup (IpcCall::dyn, PDCC_IPC_DYN), at least
 // kDynMinRows rows, at most kDynMaxChunks chunks (a function of the call's shape and a group-wide
 // setting only: identical on every rank)
-__host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid, uint32_t per) {
+__host__ __device__ inline uint32_t dyn_rows_per_chunk(size_t nrows, uint32_t grid, uint32_t per,
+                                                      uint32_t min_rows = 0) {
   size_t k = nrows / ((size_t)(per ? per : 1) * (size_t)(grid ? grid : 1));
-  if (k < kDynMinRows) k = kDynMinRows;
+  const size_t lo_rows = min_rows ? min_rows : kDynMinRows;
+  if (k < lo_rows) k = lo_rows;
   const size_t lo = (nrows + kDynMaxChunks - 1) / kDynMaxChunks;
   return (uint32_t)(k < lo ? lo : k);
 }
@@ -293,10 +299,12 @@ struct IpcCallT {
   P<const ZcTable> ztab;
   int dyn;  // > 0: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol with about `dyn` chunks per
             // workgroup (see kDynOffset); staged runs ignore it
+  int dyn_min_rows;  // rows per dynamic-protocol item, at least (0 = kDynMinRows; group-wide setting)
   int test_flags;  // PDCC_TEST_IPC_FLAGS, measurements only: bit 0 = the zero-copy reductions' arrival
                    // barrier without its release / acquire (what the data hand-over costs); bits 1-2:
                    // reduce_impl.h zc pipes; bit 3 = dyn claims from the first item (round-4 claim
-                   // loop); bit 4 = dyn control words in the uncached signal area (round-4 placement)
+                   // loop); bit 4 = dyn control words in the uncached signal area (round-4 placement); bit 5 =
+                   // the call number taken after the arguments are staged (round-4 order)
 };
 using IpcCall = IpcCallT<RawPtr>;
 

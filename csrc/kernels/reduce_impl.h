@@ -475,7 +475,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
   constexpr int D = DepthFor<W>::value;
   const int me = v.rank;
   const size_t nrows = c.bytes / kTile / W;
-  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn);
+  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nrows + K - 1) / K);
   uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
   __shared__ uint32_t s_ok;
@@ -527,7 +527,7 @@ __device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCa
                                                        const PhaseTrace* tr) {
   constexpr int D = DepthFor<W>::value;
   const size_t nt = c.bytes / kTile;
-  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn);
+  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
   const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
   dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
@@ -620,11 +620,11 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
 
 template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
-                                                uint32_t seq0) {
+                                                uint32_t seq0, bool early) {
   constexpr int D = DepthFor<W>::value;
   const size_t G = gridDim.x, b = blockIdx.x;
   const int me = v.rank;
-  const uint32_t seq = block_seq(v, seq0);
+  const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
   tr.mark(12);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
@@ -696,10 +696,15 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ DView sv;
   __shared__ DCall sc;
   PhaseTrace tr(v);
-  const uint32_t seq0 = block_seq_load(v);
+  // The block's call number is taken BEFORE the arguments are staged: consuming the counter load
+  // after the gated launch's device-side exchange (block 0's remote record stores, the other blocks'
+  // polls) waited for all of those too -- 8.3 us of block 0's 16 MiB call (profiles/r5/).
+  // PDCC_TEST_IPC_FLAGS bit 5 (A/B only): the round-4 order (seq0 = the raw load, taken in the body).
+  const bool early = (c.test_flags & 32) == 0;
+  const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq0);
+  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq0, early);
   tr.finish(v);
   zx_publish_verdict(c);
 }

@@ -22,6 +22,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_ASYNC_GRID | 0 | opt-in workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; with a cap set every rank must pass the same async_op to each collective (torch treats async_op as rank-local; PDCC_DEBUG=1 checks it) (0: no cap) |
 | PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
 | PDCC_IPC_DYN | 3 | chunks per workgroup of the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier), which the autotuner races for zero-copy all_reduce keys; 0: not raced; agreed group-wide (minimum) |
+| PDCC_IPC_DYN_MIN_ROWS | 0 (= 16) | rows (W tiles each) per item of the dynamic protocols, at least: every item is its own short pipeline, so small items make them latency-bound; agreed group-wide (minimum) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
 | PDCC_AUTOTUNE_MIN / _MAX | 64K / 4T | size range the autotuner covers (outside: the static thresholds) |
@@ -88,6 +89,7 @@ class Config:
     ipc_zc: bool = True
     ipc_push: bool = True
     ipc_dyn: int = 3
+    ipc_dyn_min_rows: int = 0
     ipc_zc_min: int = 1 << 20
     ipc_ll_max: int = 256 << 10
     ipc_zc_cache: int = 16
@@ -134,7 +136,7 @@ _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_selftest": "PDCC_IPC_SELFTEST",
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
-    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_dyn": "PDCC_IPC_DYN", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_dyn": "PDCC_IPC_DYN", "ipc_dyn_min_rows": "PDCC_IPC_DYN_MIN_ROWS", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC",
     "ipc_zx": "PDCC_IPC_ZX", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S",
     "rccl_nonblocking": "PDCC_RCCL_NONBLOCKING", "autotune": "PDCC_AUTOTUNE",

@@ -517,11 +517,12 @@ def test_autotune_file_persists_decisions(tmp_path):
     first = _gpu_launch(W.autotune_probe, 2, env=env)
     assert all(first[0]["ok"]) and all(first[1]["ok"])
     lines = [ln for ln in f.read_text().splitlines() if ln.startswith("pdcc-tune v1 w2-shared-gfx950")]
-    assert len(lines) == len(first[0]["table"]) == 5, (lines, first[0]["table"])
+    # 7 keys: 64 KiB .. 16 MiB (above 4 MiB raced against the static IPC engine, verdict r4 Next #3)
+    assert len(lines) == len(first[0]["table"]) == 7, (lines, first[0]["table"])
     second = _gpu_launch(W.autotune_probe, 2, env=env)
     for r in second:
         assert all(r["ok"]), r["ok"]
-        assert [e["iters"] for e in r["table"]] == [0] * 5, r["table"]
+        assert [e["iters"] for e in r["table"]] == [0] * 7, r["table"]
         assert sorted((e["lo"], e["algo"]) for e in r["table"]) == \
             sorted((e["lo"], e["algo"]) for e in first[0]["table"])
     assert len(f.read_text().splitlines()) == len(lines)  # nothing re-raced, nothing appended
