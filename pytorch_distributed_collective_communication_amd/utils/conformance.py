@@ -529,7 +529,9 @@ def _raced_key_checks(P, g, gb, rank, W, dev, rccl_ok, zc_ok):
         e = row_for("allreduce", "Float", "SUM", n * 4)
         if e is None or not e["ipc_valid"]:
             return False
-        raced = ["ipc_us"] + (["wide_us", "ipc_wide_us"] if rccl_ok else []) + \
+        # (a wide RCCL child the runtime refused leaves the race on every rank: rccl_wide_ctas=0)
+        wide = rccl_ok and "rccl_wide_ctas=0 " not in gb.describe()
+        raced = ["ipc_us"] + (["wide_us"] if wide else []) + (["ipc_wide_us"] if rccl_ok else []) + \
                 (["staged_us", "push_us", "dyn_us"] if zc_ok else [])
         if e["ref"] != ("rccl" if rccl_ok else "ipc") or any(e[k] <= 0 for k in raced + ["ref_us"]):
             return False
