@@ -7,8 +7,12 @@ mkdir -p gpurun_out/steps
 for spec in "$@"; do
   name=${spec%%|*}; rest=${spec#*|}; to=${rest%%|*}; cmd=${rest#*|}
   echo "[steps] $name (limit ${to}s): $cmd"
+  # progress heartbeat (a quiet step, e.g. one long pytest case, is still bounded by its own limit)
+  ( t=0; while sleep 60; do t=$((t + 60)); echo "[steps] $name running ${t}s" >> "gpurun_out/steps/$name.hb"; done ) &
+  hb=$!
   timeout -k 10 "$to" bash -c "$cmd" > "gpurun_out/steps/$name.log" 2>&1
   rc=$?
+  kill $hb 2>/dev/null; wait $hb 2>/dev/null
   echo "[steps] $name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "[steps] stopping after $name"; exit $rc; fi
 done

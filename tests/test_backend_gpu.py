@@ -18,6 +18,12 @@ pytestmark = pytest.mark.gpu
 
 def _gpu_launch(fn, world, args=("cuda",), env=None, timeout_s=60):
     e = {"PDCC_IPC_TIMEOUT_HINT": "1"}
+    if world >= 5:
+        # every rank shares this one GPU: past the hardware queues the GPU maps at once (5+ processes
+        # with a comm stream each) the hardware time-slices them and every IPC call waits out a
+        # scheduling quantum for its peers (scripts/queue_slicing_probe.py, profiles/r5/) -- one
+        # queue per rank, as the shared-GPU bench rehearsals run
+        e["GPU_MAX_HW_QUEUES"] = "1"
     e.update(env or {})
     return launch(fn, world, args=args, bind_device=True, timeout_s=timeout_s, env=e, join_timeout_s=600)
 
