@@ -713,13 +713,14 @@ std::string IpcComm::describe_error(uint32_t w) {
   if (w == 0) return "none";
   if (w == kAbortWord) return "0x200: aborted by the host (watchdog / abort_group)";
   const char* what = "unknown";
-  switch (w & ~0xffu) {
+  switch (w & ~0xffu & 0xffffu) {
     case 0x100u: what = "block-pairwise barrier"; break;
     case 0x300u: what = "LL flag poll"; break;
     case 0x400u: what = "zero-copy gate wait"; break;
     case 0x800u: what = "device-side record exchange"; break;
     case 0x900u: what = "dynamic protocol departure (done word)"; break;
     case 0xA00u: what = "dynamic protocol ready word"; break;
+    case 0x1000u: what = "resolved zero-copy slot wait (block 0's exchange verdict)"; break;
     default: break;
   }
   char buf[128];

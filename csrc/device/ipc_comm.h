@@ -90,7 +90,7 @@ class IpcComm {
   // The error word's meaning: high bits = what timed out, low byte = the rank whose kernel wrote it
   //   0x100|r block-pairwise barrier   0x200 host abort          0x300|r LL flag poll
   //   0x400|r zero-copy gate wait      0x800|r device-side record exchange
-  //   0x900|r dyn departure (done)     0xA00|r dyn ready word
+  //   0x900|r dyn departure (done)     0xA00|r dyn ready word    0x1000|r resolved-slot wait
   static std::string describe_error(uint32_t w);
 
   // PDCC_IPC_TRACE=N: kernels record per-phase device timestamps of block 0 into a
