@@ -47,14 +47,6 @@ struct gp {
     return *this;
   }
 };
-// The same for a plain pointer taken from the kernel arguments (kern::IpcView): a generic pointer
-// makes every access a flat_* instruction, and an outstanding flat store (it may alias LDS) holds
-// the wave's next LDS access until it is acknowledged -- the device-side exchange's remote record
-// stores kept block 0's next LDS write waiting ~8 us (profiles/r5/, "block_seq")
-template <class T>
-__device__ __forceinline__ T* as_global(T* q) {
-  return (T*)(__attribute__((address_space(1))) T*)q;
-}
 using DView = kern::IpcViewT<gp>;  // the IPC kernels' arguments, staged in LDS
 using DCall = kern::IpcCallT<gp>;
 static_assert(sizeof(DView) == sizeof(kern::IpcView) && sizeof(DCall) == sizeof(kern::IpcCall),
@@ -430,8 +422,7 @@ __device__ __forceinline__ void stage_tiles(const char* __restrict__ src, char* 
 // gated zero-copy launch's buffer exchange hides that wait.
 template <class V>
 __device__ __forceinline__ uint32_t block_seq_load(const V& v) {
-  return threadIdx.x == 0 ? __hip_atomic_load(as_global((uint32_t*)v.counters + blockIdx.x), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
+  return threadIdx.x == 0 ? __hip_atomic_load(v.counters + blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                           : 0u;
 }
 template <class V>
@@ -439,7 +430,7 @@ __device__ __forceinline__ uint32_t block_seq(const V& v, uint32_t loaded) {
   __shared__ uint32_t s_seq;
   if (threadIdx.x == 0) {
     const uint32_t s = loaded + 1u;
-    __hip_atomic_store(as_global((uint32_t*)v.counters + blockIdx.x), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(v.counters + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_seq = s;
   }
   __syncthreads();
@@ -592,13 +583,12 @@ __device__ __forceinline__ bool gate_wait(const kern::IpcView& v, const kern::Ip
 
 // ---- device-side record exchange of a gated zero-copy launch (kern::ZcTable) ----------
 __device__ __forceinline__ uint64_t* zx_src_words(const kern::IpcView& v, int owner, int src) {
-  return as_global(reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(v.flags[owner]) + kern::kZxOffset +
-                                               (size_t)src * kern::kZxSrcBytes));
+  return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(v.flags[owner]) + kern::kZxOffset +
+                                     (size_t)src * kern::kZxSrcBytes);
 }
 __device__ __forceinline__ kern::GateSlot* zx_resolved(const kern::IpcView& v, uint64_t seq) {
-  return as_global(reinterpret_cast<kern::GateSlot*>(reinterpret_cast<char*>(v.flags[v.rank]) +
-                                                     kern::kZxResolvedOffset) +
-                   (seq % kern::kGateSlots));
+  return reinterpret_cast<kern::GateSlot*>(reinterpret_cast<char*>(v.flags[v.rank]) + kern::kZxResolvedOffset) +
+         (seq % kern::kGateSlots);
 }
 __device__ __forceinline__ uint64_t zx_tagged(uint64_t tag, uint64_t ptr) {
   return ((tag & 0xffffull) << 48) | (ptr & 0xffffffffffffull);
@@ -618,7 +608,7 @@ __device__ __forceinline__ uint32_t& zx_verdict_note() {
 // the error word is set). Returns nothing; every block reads the resolved slot.
 __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::IpcCall& c, const PhaseTrace& tr) {
   const int lane = threadIdx.x & 63, W = v.world, me = v.rank;
-  uint32_t* epw = as_global(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(v.flags[me]) + kern::kZxEpochOffset));
+  uint32_t* epw = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(v.flags[me]) + kern::kZxEpochOffset);
   uint32_t ep = 0;
   if (lane == 0) {  // only block 0 of this rank's gated kernels touches it, in stream order
     ep = __hip_atomic_load(epw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
@@ -665,7 +655,7 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
   // lookup: lanes 0-31 scan table row q = 2p, lanes 32-63 row 2p + 1; ids and bases loaded in
   // one pass (a slot's base stays put until its mapping is closed, after every launch that
   // could have read the entry: an id match never pairs with another mapping's base)
-  const kern::ZcTable* tab = as_global(c.ztab);
+  const kern::ZcTable* tab = c.ztab;
   const int half = lane >> 5, j = lane & 31;
   uint64_t cand[4], cbase[4];
 #pragma unroll
