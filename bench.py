@@ -439,6 +439,10 @@ def run_extras(world, rank, dev, native, x):
                 out["baseline_configs"] = baseline_configs(world, rank, dev, x)
             except Exception as e:
                 out["baseline_configs_error"] = f"{type(e).__name__}: {e}"[:300]
+        try:  # the autotuner's verdicts for every key the baseline rows raced (default group)
+            out["autotune_after_baselines"] = native.autotune_table()
+        except Exception:
+            pass
         if isinstance(out.get("torch_nccl"), dict) and isinstance(out.get("baseline_configs"), dict):
             out["torch_nccl"]["vs_torch_nccl"] = vs_torch_nccl(out["baseline_configs"], out["torch_nccl"])
         with section("graph_replay"):
