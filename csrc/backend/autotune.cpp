@@ -217,42 +217,42 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
       fprintf(stderr, "[pdcc r%d] autotune %s %zu B: IPC run timed out (>%lld ms); using %s for this key\n", rank_,
               coll_name((Coll)std::get<0>(key)), bytes, (long long)cfg_.autotune_spin_ms, algo_name(cands[0]));
     }
-  const std::function<void(size_t)> run_live = [&](size_t k) {
+  // Every timed run is isolated: start / stop events around it, the stream drained, then a host
+  // barrier, so no rank starts run k+1 while a peer still executes run k. Back-to-back runs of
+  // DIFFERENT engines overlapped across ranks: a rank's zero-copy kernel waited in its entry
+  // exchange for a peer still inside the previous (staged) run, and on a shared GPU its waiting
+  // workgroups slowed that run down -- the race timed the 1 GiB zero-copy broadcast at 3853 us,
+  // isolated it takes 2242 (W = 4, scripts/race_probe.py, profiles/r5/), and adopted the slower
+  // staged engine. Isolated, each engine is timed the way a collective between other work runs.
+  hipEvent_t ea = nullptr, eb = nullptr;
+  PDCC_HIP(hipEventCreate(&ea));
+  PDCC_HIP(hipEventCreate(&eb));
+  const std::function<double(size_t)> timed = [&](size_t k) {
+    PDCC_HIP(hipEventRecord(ea, s));
     if (live[k]) run(k);
+    PDCC_HIP(hipEventRecord(eb, s));
+    PDCC_HIP(hipEventSynchronize(eb));
+    const double us = elapsed_us(ea, eb);
+    shm().barrier(timeout_);
+    return us;
   };
   // 1) one timed run each: sizes the measurement (same count on every rank: MAX-reduced inputs)
-  std::vector<hipEvent_t> e1(n + 1);
-  for (auto& e : e1) PDCC_HIP(hipEventCreate(&e));
-  PDCC_HIP(hipEventRecord(e1[0], s));
-  for (size_t k = 0; k < n; ++k) {
-    run_live(k);
-    PDCC_HIP(hipEventRecord(e1[k + 1], s));
-  }
-  PDCC_HIP(hipEventSynchronize(e1[n]));
-  for (size_t k = 0; k < n; ++k) v[k] = elapsed_us(e1[k], e1[k + 1]);
-  for (auto& e : e1) hipEventDestroy(e);
+  for (size_t k = 0; k < n; ++k) v[k] = timed(k);
   shm().allreduce(v.data(), v.size(), at::kDouble, RedOpType::MAX, timeout_);
   double slow = 1.0;
   for (size_t k = 0; k < n; ++k) slow = std::max(slow, v[k]);
   const int iters = (int)std::max(3.0, std::min(25.0, std::ceil(30000.0 / slow)));
   // 2) interleaved timed runs (ref, ipc, ref, ipc, ...): drift hits both engines alike
-  std::vector<hipEvent_t> ev(iters * n + 1);
-  for (auto& e : ev) PDCC_HIP(hipEventCreate(&e));
-  PDCC_HIP(hipEventRecord(ev[0], s));
+  std::vector<std::vector<double>> t(n);
   for (int i = 0; i < iters; ++i)
-    for (size_t k = 0; k < n; ++k) {
-      run_live(k);
-      PDCC_HIP(hipEventRecord(ev[i * n + k + 1], s));
-    }
-  PDCC_HIP(hipEventSynchronize(ev[iters * n]));
+    for (size_t k = 0; k < n; ++k) t[k].push_back(timed(k));
+  hipEventDestroy(ea);
+  hipEventDestroy(eb);
   std::vector<double> med(n);
   for (size_t k = 0; k < n; ++k) {
-    std::vector<double> t;
-    for (int i = 0; i < iters; ++i) t.push_back(elapsed_us(ev[i * n + k], ev[i * n + k + 1]));
-    std::nth_element(t.begin(), t.begin() + t.size() / 2, t.end());
-    med[k] = t[t.size() / 2];
+    std::nth_element(t[k].begin(), t[k].begin() + t[k].size() / 2, t[k].end());
+    med[k] = t[k][t[k].size() / 2];
   }
-  for (auto& e : ev) hipEventDestroy(e);
   // 3) every rank adopts the same engine: slowest rank's median, any rank's mismatch
   shm().allreduce(med.data(), med.size(), at::kDouble, RedOpType::MAX, timeout_);
   size_t best = 0;
