@@ -154,3 +154,22 @@ def test_issue_order_bookkeeping_dry():
     o.leave(1)
     assert o.log()[2:] == ["write 2 2", "wait 1 2", "write 1 3"], o.log()
     assert o.users() == 2 and o.ticks() == 3 and o.waits() == 2
+
+
+def test_conformance_helpers():
+    # the bench's conformance pass: engine patterns and the fp64-referenced closeness rule
+    import torch
+
+    from pytorch_distributed_collective_communication_amd.utils import conformance as cf
+
+    assert cf._engine_matches("ipc_2shot_dyn_zc", "ipc_2shot_dyn*")
+    assert cf._engine_matches("rccl_wide", "rccl*") and cf._engine_matches("anything", "*")
+    assert not cf._engine_matches("ipc_2shot", "ipc_2shot_zc")
+    xs = [torch.tensor([1.0, -2.0, 3.0]) * (r + 1) for r in range(4)]
+    assert cf._close(sum(xs), xs, "SUM", 4, "float32")
+    assert not cf._close(sum(xs) + 1e-3, xs, "SUM", 4, "float32")
+    assert cf._close(torch.stack(xs).amax(0), xs, "MAX", 4, "float32")
+    assert cf._close(sum(xs) / 4, xs, "AVG", 4, "float32")
+    assert cf._close(torch.stack(xs).prod(0), xs, "PRODUCT", 4, "float32")
+    b = [x.to(torch.bfloat16) for x in xs]
+    assert cf._close(sum(x.float() for x in b).to(torch.bfloat16), b, "SUM", 4, "bfloat16")
