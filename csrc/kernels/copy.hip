@@ -69,16 +69,17 @@ __global__ void __launch_bounds__(256) k2_multi_copy(CopyArgs a) {
 // all-reduce (reduce_impl.h).
 template <int W>
 __device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c, char* lds, const PhaseTrace* tr) {
+  const uint32_t xb = xchg_blocks(c), G = gridDim.x - xb, b = blockIdx.x - xb;
   const size_t nt = c.bytes / kTile;
-  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
+  const uint32_t K = kern::dyn_rows_per_chunk(nt, G, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
   const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
-  dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
+  dyn_claim_loop(v, nc, c.test_flags, tr, b, G, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(v.rank + it), t0, 1, t1};
     ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
   });
-  dyn_depart(v, dep, true, c.test_flags, tr);
+  dyn_depart(v, dep, true, c.test_flags, tr, G);
 }
 
 // Zero-copy copies (IpcCall::zc): peers' user buffers are read in place; data
@@ -86,7 +87,7 @@ __device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c
 template <int W>
 __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                             uint32_t ep) {
-  const size_t G = gridDim.x, b = blockIdx.x;
+  const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
   const size_t nt = c.bytes / kTile;
   block_barrier(v, ep);
@@ -141,7 +142,7 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
 template <int W>
 __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                               uint32_t seq0, bool early) {
-  const size_t G = gridDim.x, b = blockIdx.x;
+  const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
   const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
@@ -229,14 +230,20 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<1, kCopyDepth>::kBytes];
   __shared__ DView sv;
   __shared__ DCall sc;
-  PhaseTrace tr(v);
+  const uint32_t xb = xchg_blocks(c);
+  PhaseTrace tr(v, xb);
+  if (xb && blockIdx.x == 0) {  // the exchange block (see xchg_blocks)
+    if (threadIdx.x < 64) zx_resolve(v, c, tr);
+    tr.finish_exchange(v);
+    zx_publish_verdict(c);
+    return;
+  }
   const bool early = (c.test_flags & 32) == 0;  // (see k_ipc_reduce)
   const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_copy_body<W>(sv, sc, lds, tr, seq0, early);
   tr.finish(v);
-  zx_publish_verdict(c);
 }
 
 }  // namespace dev
@@ -444,6 +451,9 @@ hipError_t ipc_launch(const IpcView& v, const IpcCall& call, hipStream_t stream)
   }
   if (c.grid_cap > 0) grid = std::min(grid, c.grid_cap);
   grid = std::min(grid, kMaxBlocks);
+  // a gated zero-copy launch with the device-side exchange: one more workgroup, block 0, does only
+  // the exchange (dev::xchg_blocks); the data blocks keep the grid every rank computes the same way
+  if (c.gate && c.ztab && !is_ll(c.coll)) grid = std::min(grid, kMaxBlocks - 1) + 1;
   if (c.coll == IpcColl::ALLREDUCE_PUSH && !c.zc && !c.gate) return hipErrorInvalidValue;
   if (is_ll(c.coll) && (c.zc || c.bytes == 0 || c.bytes > kLLMaxBytes))
     return hipErrorInvalidValue;

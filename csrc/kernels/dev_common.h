@@ -445,12 +445,14 @@ __device__ __forceinline__ uint32_t block_seq(const V& v, uint32_t loaded) {
 // demoted to scratch memory once it crosses the kernel body's many exit paths.
 struct PhaseTrace {
   const bool on;
+  const uint32_t xb;  // 1: block 0 is a gated launch's exchange block (its words 8-11 only; the data
+                      // blocks are 1..grid-1, numbered 0.. in the record, the header is data block 0's)
   __device__ __forceinline__ static uint64_t* slots() {
     __shared__ uint64_t s[kern::kTraceWords];
     return s;
   }
-  __device__ __forceinline__ explicit PhaseTrace(const kern::IpcView& view)
-      : on(view.trace != nullptr && threadIdx.x == 0) {
+  __device__ __forceinline__ explicit PhaseTrace(const kern::IpcView& view, uint32_t xchg_blocks = 0)
+      : on(view.trace != nullptr && threadIdx.x == 0), xb(xchg_blocks) {
     if (on) {
 #pragma unroll
       for (int k = 0; k < kern::kTraceWords; ++k) slots()[k] = 0;
@@ -476,16 +478,34 @@ struct PhaseTrace {
     uint64_t* t = slots();
     t[7] = __builtin_amdgcn_s_memrealtime();
     uint64_t* r = view.trace + (size_t)view.trace_slot * kern::kTraceRecWords;
-    if (blockIdx.x == 0) {
+    const uint32_t b = blockIdx.x - xb;  // data block index
+    if (b == 0) {
 #pragma unroll
-      for (int k = 0; k < kern::kTraceWords; ++k) r[k] = t[k];
+      for (int k = 0; k < kern::kTraceWords; ++k)
+        if (!xb || k < 8 || k > 11) r[k] = t[k];
     }
-    if (blockIdx.x < (unsigned)kern::kTraceBlocks) {
-      r[kern::kTraceWords + blockIdx.x] = t[5];
-      r[kern::kTraceWords + kern::kTraceBlocks + blockIdx.x] = t[7];
+    if (b < (unsigned)kern::kTraceBlocks) {
+      r[kern::kTraceWords + b] = t[5];
+      r[kern::kTraceWords + kern::kTraceBlocks + b] = t[7];
     }
   }
+  // the exchange block's part of the record: the device-side exchange's stamps (words 8-11)
+  __device__ __forceinline__ void finish_exchange(const kern::IpcView& view) const {
+    if (!on) return;
+    uint64_t* r = view.trace + (size_t)view.trace_slot * kern::kTraceRecWords;
+    for (int k = 8; k <= 11; ++k) r[k] = slots()[k];
+  }
 };
+
+// A gated zero-copy launch with the device-side exchange (kern::ZcTable) runs one more workgroup,
+// block 0, that only does the exchange: the data blocks 1..grid-1 (b = blockIdx - 1, G = grid - 1)
+// never carry its remote record stores. Run in a data block, those flat stores stayed outstanding for
+// ~8 us and held the block's next LDS access (the r4/r5 traces' "block_seq" gap), delaying that block's
+// share of the call; block 0 is dispatched first, so the data blocks' wait for its verdict always ends.
+template <class C>
+__device__ __forceinline__ uint32_t xchg_blocks(const C& c) {
+  return (c.gate && c.ztab) ? 1u : 0u;
+}
 
 // ----------------------------------------------------------------------------
 // K4: cross-GPU block-pairwise barrier.
@@ -740,9 +760,9 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
   }
 }
 
-// The verdict for the host's statistics (read when the gate slot is reused). Stored to pinned host
-// memory only when block 0 is done: a store over PCIe stays outstanding for ~15 us, and the
-// block's next counted wait (its call-number load) would sit behind it on the critical path.
+// The verdict for the host's statistics (read when the gate slot is reused), stored to pinned host
+// memory by the exchange block when its exchange is done (a store over PCIe stays outstanding for
+// ~15 us; the exchange block has nothing left to wait for).
 __device__ __forceinline__ void zx_publish_verdict(const kern::IpcCall& c) {
   if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(const_cast<uint32_t*>(&c.gate->verdict), zx_verdict_note(), __ATOMIC_RELAXED,
@@ -781,7 +801,7 @@ __device__ __forceinline__ bool zx_wait(const kern::IpcView& v, const kern::IpcC
 
 __device__ __forceinline__ void stage_args(const kern::IpcView& v, const kern::IpcCall& c, DView& sv, DCall& sc,
                                            const PhaseTrace& tr) {
-  if (c.gate && c.ztab && blockIdx.x == 0 && threadIdx.x < 64) zx_resolve(v, c, tr);
+  // (the exchange itself runs in the launch's exchange block, see xchg_blocks)
   if (threadIdx.x == 0) {
     __builtin_memcpy(&sv, &v, sizeof(DView));  // same layout, pointers retyped global
     __builtin_memcpy(&sc, &c, sizeof(DCall));

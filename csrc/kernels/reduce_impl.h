@@ -416,15 +416,15 @@ __device__ __forceinline__ uint32_t dyn_epoch(const DView& v, int flags, const P
 // smaller, so every phase-1 item (index < nc, waiting for nothing) is reached without a wait.
 // PDCC_TEST_IPC_FLAGS bit 3 (A/B only): the round-4 loop (item b, then G + the counter, claimed
 // from the first item on).
+// (b, G: this data block's index and the number of data blocks, see xchg_blocks)
 template <class Item>
 __device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, int flags, const PhaseTrace* tr,
-                                               Item&& item) {
+                                               uint32_t b, uint32_t G, Item&& item) {
   __shared__ uint32_t s_item;
   uint32_t* const claim = dyn_ctl(v, flags) + kern::kDynClaimWord;
-  const uint32_t G = gridDim.x;
   const bool old = (flags & 8) != 0;
   const uint32_t base = old ? G : 2u * G;  // first claimed item
-  uint32_t next = blockIdx.x;
+  uint32_t next = b;
   for (;;) {
     const uint64_t t0 = tr->now();
     if (threadIdx.x == 0) s_item = next;  // (waits for the claim's return)
@@ -446,7 +446,8 @@ __device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, i
 // Departure: once every block of mine is done (exit counter), the last one tells every peer, waits
 // until every peer's blocks are done too (nobody reads my tensor any more), then resets the counters
 // and publishes this call's epoch for the next dyn call.
-__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok, int flags, const PhaseTrace* tr) {
+__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok, int flags, const PhaseTrace* tr,
+                                           uint32_t G) {
   const int me = v.rank, W = v.world;
   uint32_t* const ctl = dyn_ctl(v, flags);
   const uint64_t t0 = tr->now();
@@ -454,7 +455,7 @@ __device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t old = __hip_atomic_fetch_add(ctl + kern::kDynExitWord, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1) {
+    if (old == G - 1) {
       for (int q = 0; q < W; ++q)
         if (q != me)
           __hip_atomic_store(dyn_words(v, q, kern::kDynDoneOffset) + me, dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -474,14 +475,15 @@ template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c, char* lds, const PhaseTrace* tr) {
   constexpr int D = DepthFor<W>::value;
   const int me = v.rank;
+  const uint32_t xb = xchg_blocks(c), G = gridDim.x - xb, b = blockIdx.x - xb;
   const size_t nrows = c.bytes / kTile / W;
-  const uint32_t K = kern::dyn_rows_per_chunk(nrows, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
+  const uint32_t K = kern::dyn_rows_per_chunk(nrows, G, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nrows + K - 1) / K);
   uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
   __shared__ uint32_t s_ok;
   const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
   bool ok = true;
-  dyn_claim_loop(v, nc * W, c.test_flags, tr, [&](uint32_t it) {
+  dyn_claim_loop(v, nc * W, c.test_flags, tr, b, G, [&](uint32_t it) {
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
@@ -516,7 +518,7 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
       }
     }
   });
-  dyn_depart(v, dep, ok, c.test_flags, tr);
+  dyn_depart(v, dep, ok, c.test_flags, tr, G);
 }
 
 // Dynamic zero-copy reduce-scatter (IpcCall::dyn): my output chunk in items of K tiles, each reduced
@@ -526,16 +528,17 @@ template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCall& c, char* lds,
                                                        const PhaseTrace* tr) {
   constexpr int D = DepthFor<W>::value;
+  const uint32_t xb = xchg_blocks(c), G = gridDim.x - xb, b = blockIdx.x - xb;
   const size_t nt = c.bytes / kTile;
-  const uint32_t K = kern::dyn_rows_per_chunk(nt, gridDim.x, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
+  const uint32_t K = kern::dyn_rows_per_chunk(nt, G, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
   const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
-  dyn_claim_loop(v, nc, c.test_flags, tr, [&](uint32_t it) {
+  dyn_claim_loop(v, nc, c.test_flags, tr, b, G, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const AllSrcMap<W> m{&v, (size_t)v.rank * c.zstride, (char*)c.out[0], c.bytes, t0, 1, t1};
     ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
   });
-  dyn_depart(v, dep, true, c.test_flags, tr);
+  dyn_depart(v, dep, true, c.test_flags, tr, G);
 }
 
 // Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
@@ -548,7 +551,7 @@ template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                               uint32_t ep) {
   constexpr int D = DepthFor<W>::value;
-  const size_t G = gridDim.x, b = blockIdx.x;
+  const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
   const size_t nt = c.bytes / kTile;
   if (c.test_flags & 1) block_barrier<false>(v, ep, &tr);  // (measurement hook, see IpcCall::test_flags)
@@ -622,7 +625,7 @@ template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
                                                 uint32_t seq0, bool early) {
   constexpr int D = DepthFor<W>::value;
-  const size_t G = gridDim.x, b = blockIdx.x;
+  const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
   const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
@@ -695,18 +698,23 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
   __shared__ __attribute__((aligned(16))) char lds[PipeLds<W, DepthFor<W>::value>::kBytes];
   __shared__ DView sv;
   __shared__ DCall sc;
-  PhaseTrace tr(v);
-  // The block's call number is taken BEFORE the arguments are staged: consuming the counter load
-  // after the gated launch's device-side exchange (block 0's remote record stores, the other blocks'
-  // polls) waited for all of those too -- 8.3 us of block 0's 16 MiB call (profiles/r5/).
-  // PDCC_TEST_IPC_FLAGS bit 5 (A/B only): the round-4 order (seq0 = the raw load, taken in the body).
+  const uint32_t xb = xchg_blocks(c);
+  PhaseTrace tr(v, xb);
+  if (xb && blockIdx.x == 0) {  // the exchange block (see xchg_blocks)
+    if (threadIdx.x < 64) zx_resolve(v, c, tr);
+    tr.finish_exchange(v);
+    zx_publish_verdict(c);
+    return;
+  }
+  // The block's call number is taken at entry, before the arguments are staged (PDCC_TEST_IPC_FLAGS
+  // bit 5, A/B only: the round-4 order -- seq0 = the raw load, taken in the body; no measurable
+  // difference, profiles/r5/seq_early_ab.jsonl).
   const bool early = (c.test_flags & 32) == 0;
   const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
   ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq0, early);
   tr.finish(v);
-  zx_publish_verdict(c);
 }
 
 // ----------------------------------------------------------------------------
