@@ -95,6 +95,7 @@ Config Config::from_env() {
     c.ipc_zc_cache = (size_t)kern::kZcTab;
   }
   c.ipc_zx = env_bool("PDCC_IPC_ZX", c.ipc_zx);
+  c.ipc_zc_size_guard = env_bool("PDCC_IPC_ZC_SIZE_GUARD", c.ipc_zc_size_guard);
   c.ipc_async_grid = std::min(1024, std::max(0, env_int("PDCC_IPC_ASYNC_GRID", c.ipc_async_grid)));
   c.ipc_zc_async = env_bool("PDCC_IPC_ZC_ASYNC", c.ipc_zc_async);
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);
@@ -182,7 +183,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_dyn_min_rows=" << ipc_dyn_min_rows << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_zc_size_guard=" << ipc_zc_size_guard << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_dyn_min_rows=" << ipc_dyn_min_rows << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms << " rccl_nonblocking=" << rccl_nonblocking
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")

@@ -63,6 +63,9 @@ struct Config {
   // Device-side record exchange of gated zero-copy calls (kern::ZcTable). Every rank's intent
   // is voted on at the group's first GPU use (AND), so ranks with different settings agree.
   bool ipc_zx = true;                      // PDCC_IPC_ZX
+  // Zero-copy refuses buffers whose allocation size has bit 31 set: mapping them in a peer stalls
+  // (IpcComm::zc_export); they run staged. 0 lifts the guard (a runtime that maps them).
+  bool ipc_zc_size_guard = true;           // PDCC_IPC_ZC_SIZE_GUARD
   // Workgroup cap of IPC / LL launches issued on the comm stream (async_op=True collectives,
   // e.g. DDP / ZeRO buckets overlapped with backward): the kernels spin in cross-GPU
   // barriers while a peer lags, holding CU slots that the overlapped GEMMs need. 0 = no cap

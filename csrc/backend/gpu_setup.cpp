@@ -322,6 +322,7 @@ IpcComm& ProcessGroupMI355X::ipc(DeviceState& ds) {
     c->set_grid_max(cfg_.ipc_grid);
     c->set_async_grid(cfg_.ipc_async_grid);
     c->set_zx(ds.zx_ok);
+    c->set_zc_size_guard(cfg_.ipc_zc_size_guard);
     std::lock_guard<std::mutex> lk(init_mu_);
     ds.ipc = c;
   }
@@ -352,6 +353,7 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
                                        (uint64_t)spin_ms, ds.shared_device, cfg_.ipc_zc_cache);
     ds.ipc->set_grid_max(cfg_.ipc_grid);
     ds.ipc->set_async_grid(cfg_.ipc_async_grid);
+    ds.ipc->set_zc_size_guard(cfg_.ipc_zc_size_guard);
   } catch (const std::exception& e) {
     ok = false;
     why = e.what();

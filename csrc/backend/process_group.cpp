@@ -636,6 +636,7 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_mappings=" << (kv.second->ipc ? kv.second->ipc->zc_mappings() : 0)
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
       << ", zc_full_refusals=" << (kv.second->ipc ? kv.second->ipc->zc_full_refusals() : 0)
+      << ", zc_size_refusals=" << (kv.second->ipc ? kv.second->ipc->zc_size_refusals() : 0)
       << ", async_capped=" << (kv.second->ipc ? kv.second->ipc->async_capped() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
       << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0);

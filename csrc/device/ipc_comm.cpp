@@ -372,6 +372,16 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
   }
   const uint64_t off = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<char*>(base));
   if (off + len > range) return r;  // the readable span must lie inside one allocation
+  // An allocation whose size has bit 31 set (2-4 GiB, 6-8 GiB, ...) is never exported: a peer's
+  // hipIpcOpenMemHandle of it does not return (this ROCm 7 image, dmabuf IPC) -- the exchange stalls and
+  // every rank's gated kernels spin to their timeout, or, exchanging on the caller's thread, the group
+  // hangs. Measured with one process per rank on one MI355X (scripts/ag_probe.py, profiles/r5/
+  // zc_size_rule.md): 1024 / 2046 / 4096 / 5120 / 8192 MiB inputs map at once; 2048 / 2050 / 3072 /
+  // 6144 MiB stall. Such a buffer runs the staged protocol (PDCC_IPC_ZC_SIZE_GUARD=0 lifts the guard).
+  if (size_guard_ && (range & (size_t{1} << 31)) != 0) {
+    ++size_refusals_;
+    return r;
+  }
   uint64_t id = 0;
   if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base) != hipSuccess || id == 0) {
     (void)hipGetLastError();

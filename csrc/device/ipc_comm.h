@@ -180,6 +180,9 @@ class IpcComm {
   void reap_closing(bool wait_all);
   // fresh exports refused / not made because some rank's closing list was full (describe())
   uint64_t zc_full_refusals() const { return full_refusals_.load(); }
+  // exports refused because the allocation's size has bit 31 set (see zc_export)
+  uint64_t zc_size_refusals() const { return size_refusals_.load(); }
+  void set_zc_size_guard(bool on) { size_guard_ = on; }
   size_t zc_closing_limit() const { return closing_limit_; }
 
  private:
@@ -268,6 +271,8 @@ class IpcComm {
   size_t closing_limit_ = 16;
   std::atomic<bool> peer_full_{false};      // some rank reported `full` in the last exchange
   std::atomic<uint64_t> full_refusals_{0};
+  std::atomic<uint64_t> size_refusals_{0};
+  bool size_guard_ = true;
   mutable std::mutex imports_mu_;  // zc_imports_ (launcher thread imports, describe() counts)
   static thread_local bool tls_defer_frees_;
   std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread

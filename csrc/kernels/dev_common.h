@@ -648,7 +648,7 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
     zx_put(d + 3, (uint32_t)(c.zx_off >> 32), ep);
   }
   uint64_t id = 0, off = 0;
-  bool got = lane >= W, alive = true;
+  bool got = lane >= W, alive = true, timed_out = false;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (uint32_t it = 1;; ++it) {
     if (!got) {
@@ -664,8 +664,8 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
       }
     }
     if (__all(got)) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks ||
-        ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
+    timed_out = __builtin_amdgcn_s_memrealtime() - t0 > v.timeout_ticks;
+    if (timed_out || ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
       alive = false;
       break;
     }
@@ -734,7 +734,8 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
         }
       }
       if (__all(have)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t1 > v.timeout_ticks ||
+      timed_out = __builtin_amdgcn_s_memrealtime() - t1 > v.timeout_ticks;
+      if (timed_out ||
           ((it & 255u) == 0 && __hip_atomic_load(v.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u)) {
         alive = false;
         break;
@@ -744,7 +745,9 @@ __device__ __forceinline__ void zx_resolve(const kern::IpcView& v, const kern::I
     all_ok = alive && __all(yes);
   }
   tr.mark(10);
-  if (!alive && lane == 0) __hip_atomic_store(v.err, 0x800u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // (only this wait's own timeout is filed: a word another block or the host set first names the
+  // cause, and overwriting it hid a stalled host exchange behind "record exchange timed out")
+  if (timed_out && lane == 0) __hip_atomic_store(v.err, 0x800u | (uint32_t)me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // publish for the kernel's blocks: every word carries this launch's tag (ptr words in their
   // top 16 bits -- virtual addresses are 48-bit -- the verdict as seq = tag << 2 | verdict), so
   // readers check each word and no write ordering (no fence) is needed

@@ -95,6 +95,7 @@ class Config:
     ipc_zc_cache: int = 16
     ipc_zc_async: bool = True
     ipc_zx: bool = True
+    ipc_zc_size_guard: bool = True
     ipc_async_grid: int = 0
     ipc_spin_ms: int = 600000
     ipc_grid: int = 512
@@ -138,7 +139,7 @@ _ENV = {
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
     "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_dyn": "PDCC_IPC_DYN", "ipc_dyn_min_rows": "PDCC_IPC_DYN_MIN_ROWS", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC",
-    "ipc_zx": "PDCC_IPC_ZX", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S",
+    "ipc_zx": "PDCC_IPC_ZX", "ipc_zc_size_guard": "PDCC_IPC_ZC_SIZE_GUARD", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S",
     "rccl_nonblocking": "PDCC_RCCL_NONBLOCKING", "autotune": "PDCC_AUTOTUNE",
     "autotune_min": "PDCC_AUTOTUNE_MIN", "autotune_max": "PDCC_AUTOTUNE_MAX", "world1_local": "PDCC_WORLD1_LOCAL",
     "ipc_spin_ms": "PDCC_IPC_SPIN_MS", "ipc_grid": "PDCC_IPC_GRID", "ipc_wide_grid": "PDCC_IPC_WIDE_GRID", "autotune_sample": "PDCC_AUTOTUNE_SAMPLE",

@@ -600,6 +600,19 @@ def test_zero_copy_churn_without_barrier_stays_bounded():
         assert r["fast"][-1] > r["fast"][1] > 0, r
 
 
+def test_zero_copy_refuses_allocations_with_size_bit31():
+    # round 5: a peer's hipIpcOpenMemHandle of an allocation whose size has bit 31 set (2-4 GiB,
+    # 6-8 GiB) does not return on this image -- the W = 4..7 bench rehearsals' 2 GiB ZeRO all-gather
+    # rows stalled to the spin timeout (scripts/ag_probe.py, profiles/r5/zc_size_rule.md). Such a
+    # buffer runs staged (describe: zc_size_refusals); the next 64 MiB call maps zero-copy again.
+    env = {"PDCC_ALGO": "ipc", "PDCC_AUTOTUNE": "0"}
+    for r in _gpu_launch(W.zc_size_guard_probe, 2, env=env, timeout_s=30):
+        assert r["big_ok"] and r["small_ok"], r
+        assert r["big_s"] < 10.0, r  # (stalled: the 30 s spin timeout)
+        assert r["big_refusals"] >= 1 and r["small_refusals"] == r["big_refusals"], r
+        assert r["small_engine"].endswith("_zc"), r
+
+
 def test_zero_copy_device_exchange_epoch_wraps():
     # the device-side exchange's per-rank epoch wraps from 2^32-1 to 1
     # (never 0, and the STORED word moves on too); before the fix two consecutive calls shared
