@@ -96,6 +96,13 @@ Config Config::from_env() {
   }
   c.ipc_zx = env_bool("PDCC_IPC_ZX", c.ipc_zx);
   c.ipc_zc_size_guard = env_bool("PDCC_IPC_ZC_SIZE_GUARD", c.ipc_zc_size_guard);
+  if (c.ipc_zc_size_guard && c.ipc_max_staging >= (size_t{1} << 31)) {
+    // the staging buffer is exported and mapped like a zero-copy buffer: a 2 GiB+ window could take
+    // a size with bit 31 set, whose mapping stalls (IpcComm::zc_export)
+    fprintf(stderr, "[pdcc] PDCC_IPC_MAX_STAGING=%zu: staging stays below 2 GiB while PDCC_IPC_ZC_SIZE_GUARD=1: "
+            "clamped to 1 GiB\n", c.ipc_max_staging);
+    c.ipc_max_staging = size_t{1} << 30;
+  }
   c.ipc_async_grid = std::min(1024, std::max(0, env_int("PDCC_IPC_ASYNC_GRID", c.ipc_async_grid)));
   c.ipc_zc_async = env_bool("PDCC_IPC_ZC_ASYNC", c.ipc_zc_async);
   c.autotune = env_bool("PDCC_AUTOTUNE", c.autotune);

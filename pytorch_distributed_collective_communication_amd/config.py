@@ -20,6 +20,7 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_LL_MAX | 256K | collectives up to this size per rank / chunk (max 256K) use the LL protocol (flag-tagged pushes into the peers' signal areas, no staging copy, no barrier); 0: off |
 | PDCC_IPC_GRID | 512 | workgroup cap of the IPC kernels on distinct GPUs (1..1024; ranks sharing a GPU: 256 / W) |
 | PDCC_IPC_ASYNC_GRID | 0 | opt-in workgroup cap of the IPC/LL launches of async collectives (comm stream, overlapped with compute): leaves CU slots to the overlapped kernels; with a cap set every rank must pass the same async_op to each collective (torch treats async_op as rank-local; PDCC_DEBUG=1 checks it) (0: no cap) |
+| PDCC_IPC_ZC_SIZE_GUARD | 1 | zero-copy refuses buffers whose allocation size has bit 31 set (2-4 GiB, 6-8 GiB: a peer's mapping of them stalls on this ROCm image); they run staged, and PDCC_IPC_MAX_STAGING stays below 2 GiB |
 | PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
 | PDCC_IPC_DYN | 3 | chunks per workgroup of the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier), which the autotuner races for zero-copy all_reduce keys; 0: not raced; agreed group-wide (minimum) |
 | PDCC_IPC_DYN_MIN_ROWS | 0 (= 16) | rows (W tiles each) per item of the dynamic protocols, at least: every item is its own short pipeline, so small items make them latency-bound; agreed group-wide (minimum) |
