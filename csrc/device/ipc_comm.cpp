@@ -116,6 +116,9 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
   if (const char* tf = std::getenv("PDCC_TEST_IPC_FLAGS")) test_flags_ = std::atoi(tf);
+  shared_grid_ = std::max(1, 256 / std::max(1, world));
+  if (const char* sg = std::getenv("PDCC_TEST_SHARED_GRID"))  // A/B hook (same value on every rank)
+    shared_grid_ = std::max(1, std::min(512 / std::max(1, world) - 1, std::atoi(sg)));
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   closing_limit_ = std::max<size_t>(2, (size_t)kern::kZcTab > zc_cache_ ? (size_t)kern::kZcTab - zc_cache_ : 0);
   if (world < 2 || world > kern::kMaxRanks)
@@ -335,7 +338,7 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
   if (shared_device_) {
     // all ranks' grids must be co-resident on ONE device (test setups): stay well
     // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
-    call.grid_cap = std::max(1, 256 / world_);
+    call.grid_cap = shared_grid_;
   } else if (grid_max_ > 0 && call.grid_cap <= 0) {  // (a call may carry its own cap: IPC_WIDE)
     call.grid_cap = grid_max_;
   }

@@ -291,6 +291,7 @@ class IpcComm {
   bool shared_device_;
   int grid_max_ = 0;  // 0: the kernel library's default cap
   int async_grid_ = 0;
+  int shared_grid_ = 128;  // workgroup cap of every launch when ranks share a device (256 / W)
   bool async_now_ = false;     // inside an AsyncScope (the group's issuing thread)
   uint64_t async_capped_ = 0;  // launches the async cap applied to
 
