@@ -117,8 +117,9 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
   if (const char* tf = std::getenv("PDCC_TEST_IPC_FLAGS")) test_flags_ = std::atoi(tf);
   shared_grid_ = std::max(1, 256 / std::max(1, world));
-  if (const char* sg = std::getenv("PDCC_TEST_SHARED_GRID"))  // A/B hook (same value on every rank)
-    shared_grid_ = std::max(1, std::min(512 / std::max(1, world) - 1, std::atoi(sg)));
+  shared_wide_grid_ = std::max(1, kSharedWideSlots / std::max(1, world) - 1);
+  if (const char* sg = std::getenv("PDCC_TEST_SHARED_GRID"))  // A/B hook (same value on every rank): one cap
+    shared_grid_ = shared_wide_grid_ = std::max(1, std::min(512 / std::max(1, world) - 1, std::atoi(sg)));
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   closing_limit_ = std::max<size_t>(2, (size_t)kern::kZcTab > zc_cache_ ? (size_t)kern::kZcTab - zc_cache_ : 0);
   if (world < 2 || world > kern::kMaxRanks)
@@ -336,9 +337,12 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
   ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
   call.test_flags = test_flags_;
   if (shared_device_) {
-    // all ranks' grids must be co-resident on ONE device (test setups): stay well
-    // below the 2-workgroups-per-CU x 256-CU residency of the IPC kernels
-    call.grid_cap = shared_grid_;
+    // All ranks' grids run on ONE device (test setups, rehearsals): small calls at 256 / W workgroups per
+    // rank; from kSharedWideMin bytes per launch W x (cap + exchange block) = kSharedWideSlots in all, within
+    // the 2-per-CU x 256-CU residency of the heaviest IPC kernels (65 KiB of LDS at W = 8). More workgroups
+    // keep more loads in flight: 1 GiB all_reduce 1411 -> 1180 us (W = 2), 3842 -> 2831 (W = 4, static),
+    // 6745 -> 5156 (W = 8); calls of 4-16 MiB lose 5-15 % with them (scripts/gpu_r5_u.sh, profiles/r5/)
+    call.grid_cap = call.bytes >= kSharedWideMin ? shared_wide_grid_ : shared_grid_;
   } else if (grid_max_ > 0 && call.grid_cap <= 0) {  // (a call may carry its own cap: IPC_WIDE)
     call.grid_cap = grid_max_;
   }

@@ -291,7 +291,12 @@ class IpcComm {
   bool shared_device_;
   int grid_max_ = 0;  // 0: the kernel library's default cap
   int async_grid_ = 0;
-  int shared_grid_ = 128;  // workgroup cap of every launch when ranks share a device (256 / W)
+  // workgroup caps of the launches when ranks share a device: 256 / W, and kSharedWideSlots / W - 1 per
+  // rank from kSharedWideMin bytes (see launch_view)
+  static constexpr int kSharedWideSlots = 448;
+  static constexpr size_t kSharedWideMin = size_t{32} << 20;
+  int shared_grid_ = 128;
+  int shared_wide_grid_ = 223;
   bool async_now_ = false;     // inside an AsyncScope (the group's issuing thread)
   uint64_t async_capped_ = 0;  // launches the async cap applied to
 
