@@ -107,7 +107,11 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
   hp_.lap(HostStage::ZC_EXPORT);
   const uint64_t t = ic.gate_reserve();
   hp_.lap(HostStage::ZC_RESERVE);
-  size_t chunk = std::min(per_call_max, kGateChunk) / unit * unit;
+  static const size_t gate_chunk = [] {  // PDCC_TEST_GATE_CHUNK: A/B hook (same value on every rank)
+    const char* e = std::getenv("PDCC_TEST_GATE_CHUNK");
+    return e ? std::max<size_t>(size_t{1} << 20, std::strtoull(e, nullptr, 0)) : kGateChunk;
+  }();
+  size_t chunk = std::min(per_call_max, gate_chunk) / unit * unit;
   if (chunk == 0) chunk = unit;
   for (size_t off = 0; off < body; off += chunk) {
     kern::IpcCall c = call;

@@ -154,14 +154,18 @@ def main():
             rd, wr = W * S * (1 + (W - 1) / W), W * S
         else:
             rd, wr = W * S * (2 + (W - 1) / W), W * S * (1 + 1 + 1 / W)
+        # the trace is per launch: a zero-copy call above 256 MiB runs as launches of at most 256 MiB
+        # (launcher.cpp kGateChunk), so the rates below are per launch
+        per = min(S, 256 << 20) / S if mode == "zc" else 1.0
         for r in res:
-            r.update(mode=mode, algo=a.algo, world_on_one_gpu=W, bytes=S, hbm_read_bytes=int(rd), hbm_write_bytes=int(wr))
+            r.update(mode=mode, algo=a.algo, world_on_one_gpu=W, bytes=S, hbm_read_bytes=int(rd), hbm_write_bytes=int(wr),
+                     launch_fraction=per)
             kt = r["phases_us"]["kernel_total"]
             if kt:
-                r["hbm_TBps_kernel"] = round((rd + wr) / (kt * 1e-6) / 1e12, 2)
+                r["hbm_TBps_kernel"] = round(per * (rd + wr) / (kt * 1e-6) / 1e12, 2)
             p1 = r["phases_us"]["phase1_reduce"]
             if p1:  # phase 1 alone: every rank reads W slices of S/W and writes S/W
-                r["hbm_TBps_phase1"] = round(W * (S + S / W) / (p1 * 1e-6) / 1e12, 2)
+                r["hbm_TBps_phase1"] = round(per * W * (S + S / W) / (p1 * 1e-6) / 1e12, 2)
             print(json.dumps(r), flush=True)
 
 
