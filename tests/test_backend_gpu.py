@@ -666,3 +666,12 @@ def test_mixed_async_op_with_cap_is_caught_by_debug():
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ASYNC_GRID": "16", "PDCC_DEBUG": "1"}
     for r in _gpu_launch(W.mixed_async_op, 2, args=("cuda", True), env=env, timeout_s=120):
         assert "async_op differs" in r["error"], r
+
+@pytest.mark.parametrize("mib,blocks", [(8, 128), (64, 223)])
+def test_shared_device_grid_widens_for_large_calls(mib, blocks):
+    # ranks sharing a GPU: 256 / W workgroups per rank below 32 MiB per launch, 448 / W - 1 from there
+    # (IpcComm::launch_view; 1 GiB all_reduce 1411 -> 1213 us at W = 2, profiles/r5/shared_grid_sweep.jsonl)
+    env = {"PDCC_ALGO": "ipc", "PDCC_IPC_TRACE": "16", "PDCC_AUTOTUNE": "0"}
+    for r in _gpu_launch(W.phase_trace_probe, 2, args=("cuda", 3, mib), env=env, timeout_s=120):
+        assert r["ok"] and r["engine"].startswith("ipc_2shot"), r
+        assert r["blocks_exit"] == blocks and r["blocks_phase1"] == blocks, r
