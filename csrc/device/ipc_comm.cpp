@@ -340,8 +340,8 @@ void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_
     // All ranks' grids run on ONE device (test setups, rehearsals): small calls at 256 / W workgroups per
     // rank; from kSharedWideMin bytes per launch W x (cap + exchange block) = kSharedWideSlots in all, within
     // the 2-per-CU x 256-CU residency of the heaviest IPC kernels (65 KiB of LDS at W = 8). More workgroups
-    // keep more loads in flight: 1 GiB all_reduce 1411 -> 1180 us (W = 2), 3842 -> 2831 (W = 4, static),
-    // 6745 -> 5156 (W = 8); calls of 4-16 MiB lose 5-15 % with them (scripts/gpu_r5_u.sh, profiles/r5/)
+    // keep more loads in flight: 1 GiB all_reduce 1411 -> 1213 us (W = 2), 3842 -> 2850 (W = 4, static),
+    // 6745 -> 5140 (W = 8); calls of 4-16 MiB lose 5-15 % with them (profiles/r5/shared_grid_*.jsonl)
     call.grid_cap = call.bytes >= kSharedWideMin ? shared_wide_grid_ : shared_grid_;
   } else if (grid_max_ > 0 && call.grid_cap <= 0) {  // (a call may carry its own cap: IPC_WIDE)
     call.grid_cap = grid_max_;
