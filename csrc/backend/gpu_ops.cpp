@@ -143,12 +143,11 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
 void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                                  size_t per_call_max, hipStream_t s, const char* selftest) {
   size_t body = 0;
-  bool exported = true;  // (a gated call: this rank's buffer could be exported, e.g. not size-guarded)
   if (!selftest && !staged_only_ && cfg_.ipc_zc_async && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
       !capturing(s)) {
     // gated launches now, the exchange on the exchange thread (launcher.cpp)
     body = call.bytes / unit * unit;
-    if (body) exported = ipc_gated(ds, call, zbuf, zlen, unit, body, per_call_max, s);
+    if (body) ipc_gated(ds, call, zbuf, zlen, unit, body, per_call_max, s);
   } else {
     if (!selftest) launcher_quiesce(ds);  // inline exchange: the channel is this thread's now
     body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
@@ -156,7 +155,7 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
   if (!selftest) {  // recorded as zero-copy if this rank shares its buffer (a gated call whose
                    // exchange fails on another rank runs staged: describe() "zc_fallbacks")
     std::lock_guard<std::mutex> lk(stats_mu_);
-    zc_ran_ = body > 0 && exported && (zbuf != nullptr || zlen == 0);
+    zc_ran_ = body > 0 && (zbuf != nullptr || zlen == 0);
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;

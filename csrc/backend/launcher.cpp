@@ -99,7 +99,7 @@ host::ShmComm& ProcessGroupMI355X::exchange_channel(DeviceState& ds) {
 // so that the staged fallback of each fits a staging window of at most kGateChunk.
 constexpr size_t kGateChunk = 256u << 20;
 
-bool ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen,
+void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen,
                                    size_t unit, size_t body, size_t per_call_max, hipStream_t s) {
   IpcComm& ic = ipc(ds);
   hp_.lap(HostStage::ENQUEUE);
@@ -182,7 +182,6 @@ bool ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
   L.pushed.fetch_add(1, std::memory_order_release);
   L.cv.notify_one();
   hp_.lap(HostStage::ZC_JOB);
-  return mine.ok != 0;
 }
 
 void ProcessGroupMI355X::stop_launchers() {

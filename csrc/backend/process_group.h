@@ -471,9 +471,8 @@ class ProcessGroupMI355X : public c10d::Backend {
   // the staged rest is the same call with every in/out pointer moved past the body.
   void ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                size_t per_call_max, hipStream_t s, const char* selftest = nullptr);
-  // zero-copy body of `call` as gated launches on `s` + the exchange job (launcher.cpp); false if this
-  // rank could not export its buffer (the launches then run staged on every rank)
-  bool ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen, size_t unit, size_t body,
+  // zero-copy body of `call` as gated launches on `s` + the exchange job (launcher.cpp)
+  void ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen, size_t unit, size_t body,
                  size_t per_call_max, hipStream_t s);
   IpcLauncher& launcher(DeviceState& ds);
   void launcher_loop(DeviceState* ds, IpcLauncher* l);
