@@ -379,9 +379,10 @@ def rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args):
         return {"skipped": f"ranks share a GPU ({world} ranks, {ngpu} GPU): RCCL refuses duplicate devices"}
     if os.environ.get("PDCC_BENCH_RCCL_ENV_SWEEP", "1") == "0":
         return {"skipped": "PDCC_BENCH_RCCL_ENV_SWEEP=0"}
-    if any(os.environ.get(k) for k in ("NCCL_BUFFSIZE", "NCCL_PROTO", "PDCC_RCCL_BUFFSIZE", "PDCC_RCCL_PROTO")):
-        return {"skipped": "NCCL_BUFFSIZE / NCCL_PROTO set by the user"}
     from pytorch_distributed_collective_communication_amd.utils import rccl_env
+
+    if rccl_env.user_set():
+        return {"skipped": f"RCCL settings made by the user: {rccl_env.user_set()}"}
 
     if rank == 0:
         print("[bench] RCCL environment pre-sweep (fresh child ranks per point)", file=sys.stderr, flush=True)
@@ -391,7 +392,7 @@ def rccl_env_presweep(store, rank, world, local, on_gpu, ngpu, args):
     except Exception as e:  # never in the way of the headline
         return {"error": f"{type(e).__name__}: {e}"[:300]}
     for k, v in env.items():
-        os.environ[k] = v  # before this process's first RCCL communicator
+        os.environ[rccl_env._PDCC_NAME[k]] = v  # before this process's first RCCL communicator
     return rec
 
 
@@ -600,8 +601,8 @@ def _group_with_env(world, env, timeout_s=60):
 
 def rccl_tuning(world, rank, dev, x):
     """RCCL on this node's xGMI (only where ranks sit on distinct GPUs):
-    * cta_sweep: 1 GiB all_reduce busbw for RCCL channel floors (minCTAs) default/28/56/112
-      -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate (the autotuner
+    * cta_sweep: 1 GiB all_reduce busbw at RCCL's default and at exactly 28/56/112 channels
+      (minCTAs = maxCTAs) -- one CTA drives one channel, and a GPU has 7 xGMI links to saturate (the autotuner
       races the 112-channel child communicator, PDCC_RCCL_WIDE_CTAS, for large keys);
     * list_all_gather: all_gather into separate tensors, grouped p2p straight into the
       list (zero copy) vs ring all_gather into staging + K2 unpack;
@@ -621,7 +622,7 @@ def rccl_tuning(world, rank, dev, x):
         progress(f"rccl cta sweep: {ctas}")
         env = {"PDCC_RCCL_GROUP_COMM": "init", "PDCC_ALGO": "rccl"}
         if ctas != "default":
-            env["PDCC_RCCL_MIN_CTAS"] = ctas
+            env["PDCC_RCCL_MIN_CTAS"] = env["PDCC_RCCL_MAX_CTAS"] = ctas  # exact counts
         g = _group_with_env(world, env)
         t = _p50_coll(lambda: dist.all_reduce(big, group=g), iters=5)
         sweep[str(ctas)] = round(bb("all_reduce", big.numel() * 4, world, t), 1)
@@ -782,9 +783,28 @@ def baseline_configs(world, rank, dev, x, group=None, engine=None):
         chunk = n // world
         xs = x[:n]
         xs.uniform_(0.0, 1e-3)
-        rec(f"all_reduce_{L}", "all_reduce", S, lambda: dist.all_reduce(xs, group=g))
-        rec(f"reduce_{L}", "reduce", S, lambda: dist.reduce(xs, dst=0, group=g))
-        rec(f"broadcast_{L}", "broadcast", S, lambda: dist.broadcast(xs, src=0, group=g))
+        tri = world * (world + 1) / 2  # sum of the fills rank + 1
+
+        def check_all_reduce(t):  # verdict r5 Next #2: a known fill through the same call shape
+            t.fill_(rank + 1.0)
+            dist.all_reduce(t, group=g)
+            return bool(torch.all(t == tri).item())
+
+        def check_reduce(t):  # root: the sum; every other rank's buffer untouched
+            t.fill_(rank + 1.0)
+            dist.reduce(t, dst=0, group=g)
+            return bool(torch.all(t == (tri if rank == 0 else rank + 1.0)).item())
+
+        def check_broadcast(t):
+            t.fill_(7.0 if rank == 0 else -1.0)
+            dist.broadcast(t, src=0, group=g)
+            return bool(torch.all(t == 7.0).item())
+
+        rec(f"all_reduce_{L}", "all_reduce", S, lambda: dist.all_reduce(xs, group=g),
+            check=lambda: check_all_reduce(xs))
+        rec(f"reduce_{L}", "reduce", S, lambda: dist.reduce(xs, dst=0, group=g), check=lambda: check_reduce(xs))
+        rec(f"broadcast_{L}", "broadcast", S, lambda: dist.broadcast(xs, src=0, group=g),
+            check=lambda: check_broadcast(xs))
         src = torch.full((chunk,), float(rank), device=dev)
         out = torch.empty(n - n % world, device=dev)
         rec(f"all_gather_{L}", "all_gather", S, lambda: dist.all_gather_into_tensor(out, src, group=g),
@@ -801,18 +821,52 @@ def baseline_configs(world, rank, dev, x, group=None, engine=None):
         rec(f"reduce_scatter_{L}", "reduce_scatter", S, lambda: dist.reduce_scatter_tensor(sout, rsin, group=g),
             check=lambda: sout[0].item() == world)
         a2a = torch.empty_like(rsin)
-        rec(f"all_to_all_{L}", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin, group=g))
+        a2a_chunk = a2a.numel() // world
+
+        def check_a2a():  # block j of rank r goes to rank j's block r: fill r * W + j, expect j * W + r
+            blocks = rsin.view(world, a2a_chunk)
+            for j in range(world):
+                blocks[j].fill_(float(rank * world + j))
+            dist.all_to_all_single(a2a, rsin, group=g)
+            want = torch.arange(world, device=dev, dtype=torch.float32) * world + rank
+            return bool(torch.all(a2a.view(world, a2a_chunk) == want[:, None]).item())
+
+        rec(f"all_to_all_{L}", "all_to_all", S, lambda: dist.all_to_all_single(a2a, rsin, group=g),
+            check=check_a2a)
         del rsin, a2a, out, src
         m = ((128 << 20) if not SMALL else (8 << 20)) // 4
+        pos = torch.arange(m, device=dev, dtype=torch.int64)
+
+        def fill_op(v, op):
+            # closed forms, position-dependent (a misplaced tile shows): PRODUCT of powers of two
+            # (exact), MAX / MIN of small integers
+            if op == "PRODUCT":
+                v.copy_(torch.exp2(((pos + rank) % 3 - 1).float()))
+            else:
+                v.copy_(((pos % 97) * world + rank).float())
+
+        def want_op(op):
+            if op == "PRODUCT":
+                e = sum(((pos + r) % 3 - 1) for r in range(world))
+                return torch.exp2(e.float())
+            return ((pos % 97) * world + (world - 1 if op == "MAX" else 0)).float()
+
+        def check_op(v, op):
+            fill_op(v, op)
+            dist.all_reduce(v, op=getattr(dist.ReduceOp, op), group=g)
+            return bool(torch.equal(v, want_op(op)))
+
         for op in ("PRODUCT", "MAX", "MIN"):
-            v = torch.full((m,), 1.0 + 1e-7 * rank, device=dev)
+            v = torch.empty(m, device=dev)
+            fill_op(v, op)
             rec(f"all_reduce_{op}_{size_label(m * 4)}", "all_reduce", m * 4,
-                lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op), group=g))
-        del v
+                lambda: dist.all_reduce(v, op=getattr(dist.ReduceOp, op), group=g),
+                check=lambda: check_op(v, op))
+        del v, pos
         if world == 2:
             n2 = min(256 << 20, x.numel() * 4) // 4
             rec(f"all_reduce_{size_label(n2 * 4)}_w2", "all_reduce", n2 * 4,
-                lambda: dist.all_reduce(x[:n2], group=g))
+                lambda: dist.all_reduce(x[:n2], group=g), check=lambda: check_all_reduce(x[:n2]))
         per = ((4 << 30) if not SMALL else (64 << 20)) // 2  # 4 GiB of bf16 per rank
         per = min(per, _shared_gpu_cap(world, dev) // 2)
         ag_in = torch.full((per,), float(rank), dtype=torch.bfloat16, device=dev)

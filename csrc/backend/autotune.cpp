@@ -49,6 +49,10 @@ std::vector<Algo> ProcessGroupMI355X::tune_candidates(Coll c, size_t bytes, bool
                         c == Coll::REDUCE_SCATTER;
   if (dyn_coll && cfg_.ipc_dyn > 0 && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min)
     v.push_back(Algo::IPC_DYN);
+  // the copy collectives on the copy engines (zero-copy sizes): no CU moves their bytes
+  const bool sdma_coll = c == Coll::BROADCAST || c == Coll::ALLGATHER || c == Coll::GATHER || c == Coll::SCATTER ||
+                         c == Coll::ALLTOALL;
+  if (sdma_coll && cfg_.ipc_sdma && zc_can && cfg_.ipc_zc && bytes >= cfg_.ipc_zc_min) v.push_back(Algo::IPC_SDMA);
   if (v.size() < 2) return {};  // nothing to race
   return v;
 }
@@ -68,7 +72,7 @@ Algo ProcessGroupMI355X::decide(Coll c, int dtype, int op, size_t bytes, DeviceS
   if (cands.empty()) return a0;
   // an async call whose IPC launches run the capped grid (PDCC_IPC_ASYNC_GRID) is a key of its own
   // (bucket + kAsyncBucket): a verdict timed at one grid is never applied at the other
-  const int bucket = size_bucket(bytes) + (op_async_ && cfg_.ipc_async_grid > 0 ? kAsyncBucket : 0);
+  const int bucket = size_bucket(bytes) + (runs_capped(ds.device) ? kAsyncBucket : 0);
   const TuneKey key{(int)c, dtype, op, bucket};
   const Algo t = tuned(key);
   const bool cap = capturing_on(ds.device);
@@ -156,7 +160,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   Spin spin(has_ipc ? ds.ipc.get() : nullptr, (uint64_t)cfg_.autotune_spin_ms, tuning_);
   // an async call's key is raced with the grid its IPC launches will run at (PDCC_IPC_ASYNC_GRID):
   // the verdict must hold for the capped engine next to compute, not for the full grid
-  IpcComm::AsyncScope async_cap(has_ipc ? ds.ipc.get() : nullptr, op_async_ && cfg_.ipc_async_grid > 0);
+  IpcComm::AsyncScope async_cap(has_ipc ? ds.ipc.get() : nullptr, runs_capped(ds.device));
   // The IPC engine as the reference (no RCCL, above kHostTuneMax): first its result on a prefix
   // of the caller's data against the host transport's, agreed on every rank. A failure (or an
   // IPC spin timeout in the reference run below) sends the key to the host engine: slow, exact.
@@ -269,6 +273,7 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
        : cands[k] == Algo::IPC_WIDE   ? te.ipc_wide_us
        : cands[k] == Algo::IPC_STAGED ? te.staged_us
        : cands[k] == Algo::IPC_DYN    ? te.dyn_us
+       : cands[k] == Algo::IPC_SDMA   ? te.sdma_us
                                       : te.push_us) = med[k];
       te.valid = te.valid && v[n + k] == 0.0;
     } else if (cands[k] == Algo::RCCL_WIDE) {
@@ -285,9 +290,9 @@ Algo ProcessGroupMI355X::autotune(const TuneKey& key, size_t bytes, DeviceState&
   if (cfg_.log_level >= 1 && rank_ == 0)
     fprintf(stderr,
             "[pdcc r0] autotune %s %zu B: %s %.1f us, rccl_wide %.1f us, ipc %.1f us, ipc_wide %.1f us, ipc_push %.1f us,"
-            " ipc_staged %.1f us, ipc_dyn %.1f us%s (%d runs each) -> %s\n",
+            " ipc_staged %.1f us, ipc_dyn %.1f us, ipc_sdma %.1f us%s (%d runs each) -> %s\n",
             coll_name((Coll)std::get<0>(key)), bytes, algo_name(cands[0]), te.rccl_us, te.wide_us, te.ipc_us,
-            te.ipc_wide_us, te.push_us, te.staged_us, te.dyn_us,
+            te.ipc_wide_us, te.push_us, te.staged_us, te.dyn_us, te.sdma_us,
             te.valid ? "" : " (MISMATCH)", iters, algo_name(te.algo));
   return te.algo;
 }
@@ -337,11 +342,11 @@ void ProcessGroupMI355X::file_append(const TuneKey& key, const TuneEntry& e, con
   }
   flock(fileno(f), LOCK_EX);
   std::fprintf(f, "pdcc-tune v1 %s %d %d %d %d %s # %s %s %zu-%zu B: ref %.1f us, rccl_wide %.1f, ipc %.1f, "
-               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f, ipc_dyn %.1f\n",
+               "ipc_wide %.1f, ipc_push %.1f, ipc_staged %.1f, ipc_dyn %.1f, ipc_sdma %.1f\n",
                tune_sig(ds).c_str(), std::get<0>(key), std::get<1>(key), std::get<2>(key), std::get<3>(key),
                algo_name(e.algo), coll_name((Coll)std::get<0>(key)), algo_name(e.ref),
                (size_t)1 << (std::get<3>(key) % kAsyncBucket), (size_t)2 << (std::get<3>(key) % kAsyncBucket), e.rccl_us, e.wide_us, e.ipc_us, e.ipc_wide_us, e.push_us, e.staged_us,
-               e.dyn_us);
+               e.dyn_us, e.sdma_us);
   std::fflush(f);
   flock(fileno(f), LOCK_UN);
   std::fclose(f);
@@ -366,6 +371,7 @@ std::vector<ProcessGroupMI355X::TuneRecord> ProcessGroupMI355X::autotune_table()
     r.ipc_wide_us = e.ipc_wide_us;
     r.staged_us = e.staged_us;
     r.dyn_us = e.dyn_us;
+    r.sdma_us = e.sdma_us;
     r.wide_us = e.wide_us;
     r.valid = e.valid;
     r.algo = algo_name(e.algo);

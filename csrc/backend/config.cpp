@@ -49,13 +49,14 @@ const char* algo_name(Algo a) {
     case Algo::IPC_WIDE: return "ipc_wide";
     case Algo::IPC_STAGED: return "ipc_staged";
     case Algo::IPC_DYN: return "ipc_dyn";
+    case Algo::IPC_SDMA: return "ipc_sdma";
   }
   return "?";
 }
 
 Algo algo_from_name(const std::string& n) {
   for (Algo a : {Algo::RCCL, Algo::IPC, Algo::HOST, Algo::IPC_PUSH, Algo::RCCL_WIDE, Algo::IPC_WIDE, Algo::IPC_STAGED,
-                 Algo::IPC_DYN})
+                 Algo::IPC_DYN, Algo::IPC_SDMA})
     if (n == algo_name(a)) return a;
   return Algo::AUTO;
 }
@@ -73,7 +74,8 @@ Config Config::from_env() {
     else if (s == "ipc_wide") c.force_algo = Algo::IPC_WIDE;
     else if (s == "ipc_staged") c.force_algo = Algo::IPC_STAGED;
     else if (s == "ipc_dyn") c.force_algo = Algo::IPC_DYN;
-    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|host, got " + s);
+    else if (s == "ipc_sdma") c.force_algo = Algo::IPC_SDMA;
+    else throw std::runtime_error("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|ipc_sdma|host, got " + s);
   }
   c.ipc_1shot_max = env_size("PDCC_IPC_1SHOT_MAX", c.ipc_1shot_max);
   c.ipc_2shot_max = env_size("PDCC_IPC_2SHOT_MAX", c.ipc_2shot_max);
@@ -85,6 +87,8 @@ Config Config::from_env() {
   c.ipc_zc = env_bool("PDCC_IPC_ZC", c.ipc_zc);
   c.ipc_push = env_bool("PDCC_IPC_PUSH", c.ipc_push);
   c.ipc_dyn = std::min(64, std::max(0, env_int("PDCC_IPC_DYN", c.ipc_dyn)));
+  c.ipc_sdma = env_bool("PDCC_IPC_SDMA", c.ipc_sdma);
+  c.sdma_streams = std::min(6, std::max(0, env_int("PDCC_SDMA_STREAMS", c.sdma_streams)));
   c.ipc_dyn_min_rows = std::min(4096, std::max(0, env_int("PDCC_IPC_DYN_MIN_ROWS", c.ipc_dyn_min_rows)));
   c.ipc_zc_min = env_size("PDCC_IPC_ZC_MIN", c.ipc_zc_min);
   c.ipc_ll_max = env_size("PDCC_IPC_LL_MAX", c.ipc_ll_max);
@@ -190,7 +194,7 @@ std::string Config::describe() const {
     << " ipc_1shot_max=" << ipc_1shot_max
     << " ipc_2shot_max=" << ipc_2shot_max << " ipc_copy_max=" << ipc_copy_max
     << " ipc_max_staging=" << ipc_max_staging << " ipc_zc=" << ipc_zc << " ipc_zc_min=" << ipc_zc_min
-    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_zc_size_guard=" << ipc_zc_size_guard << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_dyn_min_rows=" << ipc_dyn_min_rows << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
+    << " ipc_zc_cache=" << ipc_zc_cache << " ipc_zc_async=" << ipc_zc_async << " ipc_zx=" << ipc_zx << " ipc_zc_size_guard=" << ipc_zc_size_guard << " ipc_async_grid=" << ipc_async_grid << " ipc_ll_max=" << ipc_ll_max << " ipc_push=" << ipc_push << " ipc_dyn=" << ipc_dyn << " ipc_dyn_min_rows=" << ipc_dyn_min_rows << " ipc_sdma=" << ipc_sdma << " sdma_streams=" << sdma_streams << " ipc_spin_ms=" << ipc_spin_ms << " ipc_grid=" << ipc_grid << " ipc_wide_grid=" << ipc_wide_grid << " autotune=" << autotune
     << " autotune_sample=" << autotune_sample << " autotune_file=" << (autotune_file.empty() ? "-" : autotune_file) << " rccl_ctas=" << rccl_min_ctas << ".." << rccl_max_ctas << " rccl_wide_ctas=" << rccl_wide_ctas
     << " rccl_wide_min=" << rccl_wide_min << " rccl_init_timeout_ms=" << rccl_init_timeout_ms << " rccl_nonblocking=" << rccl_nonblocking
     << " group_comm=" << (group_comm == 0 ? "split" : group_comm == 1 ? "share" : "init")

@@ -20,10 +20,13 @@ namespace pdcc {
 // IPC_DYN: the zero-copy 2-shot all-reduce with work items claimed dynamically and per-chunk
 // ready words instead of fixed tile ranges and a block-pairwise barrier (kern::kDynOffset),
 // an autotuner candidate next to IPC for zero-copy all_reduce keys.
-enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE, IPC_STAGED, IPC_DYN };
+// IPC_SDMA: the copy collectives (broadcast, all_gather, gather, scatter, all_to_all) at zero-copy
+// sizes as hipMemcpyAsync pulls between IPC-mapped user buffers -- the runtime's copy engines move
+// the bytes instead of CU kernels (gpu_ops.cpp sdma_run); an autotuner candidate for those keys.
+enum class Algo : int { AUTO = 0, RCCL, IPC, HOST, IPC_PUSH, RCCL_WIDE, IPC_WIDE, IPC_STAGED, IPC_DYN, IPC_SDMA };
 inline bool is_ipc(Algo a) {
   return a == Algo::IPC || a == Algo::IPC_PUSH || a == Algo::IPC_WIDE || a == Algo::IPC_STAGED ||
-         a == Algo::IPC_DYN;
+         a == Algo::IPC_DYN || a == Algo::IPC_SDMA;
 }
 inline bool is_rccl(Algo a) { return a == Algo::RCCL || a == Algo::RCCL_WIDE; }
 
@@ -47,6 +50,11 @@ struct Config {
   // PDCC_IPC_DYN: chunks per workgroup of the dynamic 2-shot all-reduce (IPC_DYN; fewer = less
   // per-item overhead, more = finer load balance); 0: the autotuner does not race it (0..64)
   int ipc_dyn = 3;
+  // PDCC_IPC_SDMA: the autotuner races the copy-engine candidate (IPC_SDMA) for copy-collective keys
+  // of zero-copy sizes; PDCC_SDMA_STREAMS: side streams a call's pulls fan out over (0..6; each
+  // stream's copies run in order, several streams keep several copy engines busy)
+  bool ipc_sdma = true;
+  int sdma_streams = 2;
   // PDCC_IPC_DYN_MIN_ROWS: rows (W tiles each) per dynamic item, at least (0 = kern::kDynMinRows = 16;
   // 1..4096; voted group-wide like PDCC_IPC_DYN)
   int ipc_dyn_min_rows = 0;

@@ -39,6 +39,11 @@ Algo ProcessGroupMI355X::choose(Coll c, size_t bytes, DeviceState& ds, bool rccl
                  ? Algo::IPC_DYN
                  : Algo::IPC;
     if (cfg_.force_algo == Algo::IPC_STAGED && ipc_can) return Algo::IPC_STAGED;
+    if (cfg_.force_algo == Algo::IPC_SDMA && ipc_can)  // the copy collectives (the others: the IPC kernels)
+      return (c == Coll::BROADCAST || c == Coll::ALLGATHER || c == Coll::GATHER || c == Coll::SCATTER ||
+              c == Coll::ALLTOALL) && ds.zc_ok
+                 ? Algo::IPC_SDMA
+                 : Algo::IPC;
     if (ipc_can) {
       size_t lim = cfg_.ipc_copy_max;
       if (c == Coll::ALLREDUCE || c == Coll::REDUCE || c == Coll::BROADCAST) lim = cfg_.ipc_2shot_max;
@@ -78,13 +83,9 @@ void ProcessGroupMI355X::ipc_chunked(IpcComm& ic, kern::IpcCall call, size_t per
 // only, so all ranks take the same branch: the records go round the host transport
 // (a few us), a second round only when some rank exported an allocation its peers
 // have not mapped yet (agreeing that every mapping worked).
-size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen,
-                                         size_t unit, hipStream_t s, const char* selftest) {
-  if (!selftest && (staged_only_ || !ds.zc_ok || !cfg_.ipc_zc || call.bytes < cfg_.ipc_zc_min)) return 0;
-  const size_t body = call.bytes / unit * unit;
-  if (body == 0) return 0;
+bool ProcessGroupMI355X::zc_map(DeviceState& ds, const void* zbuf, size_t zlen, bool cap, const char* selftest,
+                                std::vector<char*>& ptrs) {
   IpcComm& ic = ds.ipc ? *ds.ipc : ipc(ds);
-  const bool cap = capturing(s);
   const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, cap);
   std::vector<IpcComm::ZcRec> all(size_);
   if (selftest) {  // init_mu_ is held: exchange through the store, not the host transport
@@ -105,7 +106,6 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
     all_ok = all_ok && r.ok;
     fresh = fresh || r.fresh;
   }
-  std::vector<char*> ptrs;
   bool ok = ic.zc_import(all, zbuf, all_ok, ptrs);
   if (all_ok && fresh) {
     if (selftest) {
@@ -120,7 +120,17 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
   }
   ok = ok && all_ok;
   ic.zc_settle(mine, ok);
-  if (!ok) return 0;
+  return ok;
+}
+
+size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen,
+                                         size_t unit, hipStream_t s, const char* selftest) {
+  if (!selftest && (staged_only_ || !ds.zc_ok || !cfg_.ipc_zc || call.bytes < cfg_.ipc_zc_min)) return 0;
+  const size_t body = call.bytes / unit * unit;
+  if (body == 0) return 0;
+  IpcComm& ic = ds.ipc ? *ds.ipc : ipc(ds);
+  std::vector<char*> ptrs;
+  if (!zc_map(ds, zbuf, zlen, capturing(s), selftest, ptrs)) return 0;
   if (call.coll == kern::IpcColl::REDUCE_2SHOT || call.coll == kern::IpcColl::ALLREDUCE_PUSH) {
     // the rooted reduce stages its reduced tiles, the push all-reduce receives its owned
     // tiles in staging: chunks of at most the staging cap
@@ -143,19 +153,24 @@ size_t ProcessGroupMI355X::ipc_zero_copy(DeviceState& ds, kern::IpcCall call, co
 void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void* zbuf, size_t zlen, size_t unit,
                                  size_t per_call_max, hipStream_t s, const char* selftest) {
   size_t body = 0;
-  if (!selftest && !staged_only_ && cfg_.ipc_zc_async && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
-      !capturing(s)) {
-    // gated launches now, the exchange on the exchange thread (launcher.cpp)
+  // (the same conditions ipc_zero_copy applies: a call below them is staged by design, not a fallback)
+  const bool attempt = !selftest && !staged_only_ && ds.zc_ok && cfg_.ipc_zc && call.bytes >= cfg_.ipc_zc_min &&
+                       call.bytes / unit > 0;
+  ZcPart part;
+  if (attempt && cfg_.ipc_zc_async && !capturing(s)) {
+    // gated launches now, the exchange on the exchange thread (launcher.cpp); whether they ran
+    // zero-copy or staged is known once the exchange has run (the part stays pending until then)
     body = call.bytes / unit * unit;
-    if (body) ipc_gated(ds, call, zbuf, zlen, unit, body, per_call_max, s);
+    part.ticket = ipc_gated(ds, call, zbuf, zlen, unit, body, per_call_max, s);
+    part.launcher = ds.launcher.get();
   } else {
     if (!selftest) launcher_quiesce(ds);  // inline exchange: the channel is this thread's now
     body = ipc_zero_copy(ds, call, zbuf, zlen, unit, s, selftest);
+    part.state = body > 0 ? 1 : 0;
   }
-  if (!selftest) {  // recorded as zero-copy if this rank shares its buffer (a gated call whose
-                   // exchange fails on another rank runs staged: describe() "zc_fallbacks")
+  if (attempt) {  // the op's engine label is settled from the outcome (record())
     std::lock_guard<std::mutex> lk(stats_mu_);
-    zc_ran_ = body > 0 && (zbuf != nullptr || zlen == 0);
+    zc_parts_.push_back(part);
   }
   if (body == call.bytes) return;
   kern::IpcCall rest = call;
@@ -172,6 +187,75 @@ void ProcessGroupMI355X::ipc_run(DeviceState& ds, kern::IpcCall call, const void
     if (rest.coll == kern::IpcColl::BROADCAST_2SHOT) rest.coll = kern::IpcColl::BROADCAST_1SHOT;
   }
   ipc_chunked(ipc(ds), rest, per_call_max, s);
+}
+
+// Copy-engine engine (verdict r5 Next #4, SURVEY §2.4 K3 "compare with hipMemcpyPeerAsync"). The copy
+// collectives (reference main.py:37,52,68,81; the ZeRO parameter gather README.md:254 motivates) move
+// their bytes with hipMemcpyAsync between IPC-mapped user buffers: the runtime's copy engines do the
+// work, so a gather overlapped with GEMMs leaves every CU to them. Pull only -- every byte lands in
+// memory of the GPU that issued its copy, which HIP's stream semantics then make visible to this
+// rank's later kernels (no cross-GPU cache maintenance of remote writes to reason about). Order:
+// the exchange (this thread, like an inline zero-copy call), a flags-only barrier launch (every
+// peer's earlier kernels -- the writes of what is read here -- have finished), the pulls fanned out
+// over up to PDCC_SDMA_STREAMS side streams (one stream's copies run in order), a second barrier
+// launch (no peer reads this rank's buffer any more once it passes), the mappings kept open until
+// that launch is done. Both barriers are single-workgroup IPC launches: every rank issues the same
+// IPC sequence, so the per-block call numbers stay in step with the other engines.
+bool ProcessGroupMI355X::sdma_run(
+    DeviceState& ds, const void* zbuf, size_t zlen, hipStream_t s,
+    const std::function<void(const std::vector<char*>&, std::vector<kern::CopyDesc>&)>& plan) {
+  if (!ds.zc_ok || !cfg_.ipc_zc || capturing(s)) return false;  // (group-wide facts: every rank alike)
+  launcher_quiesce(ds);  // inline exchange: the channel is this thread's now
+  IpcComm& ic = ipc(ds);
+  std::vector<char*> ptrs;
+  const bool ok = zc_map(ds, zbuf, zlen, false, nullptr, ptrs);
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    ZcPart part;
+    part.state = ok ? 1 : 0;
+    zc_parts_.push_back(part);
+  }
+  if (!ok) return false;
+  std::vector<kern::CopyDesc> copies;
+  plan(ptrs, copies);
+  copies.erase(std::remove_if(copies.begin(), copies.end(),
+                              [](const kern::CopyDesc& d) { return d.bytes == 0 || d.src == d.dst; }),
+               copies.end());
+  kern::IpcCall bar{};
+  bar.coll = kern::IpcColl::BARRIER;
+  bar.dtype = kern::DType::U8;
+  bar.op = kern::RedOp::COPY;
+  ic.launch(bar, s);  // arrival
+  const int nside = std::min<int>(cfg_.sdma_streams, (int)copies.size() - 1);
+  if (nside <= 0) {
+    for (const auto& d : copies) PDCC_HIP(hipMemcpyAsync(d.dst, d.src, d.bytes, hipMemcpyDeviceToDevice, s));
+  } else {
+    while ((int)ds.sdma_side.size() < nside) {
+      hipStream_t x = nullptr;
+      PDCC_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+      ds.sdma_side.push_back(x);
+    }
+    hipEvent_t fork = ds.events->get();
+    PDCC_HIP(hipEventRecord(fork, s));
+    for (int k = 0; k < nside; ++k) PDCC_HIP(hipStreamWaitEvent(ds.sdma_side[k], fork, 0));
+    ds.events->put(fork);
+    for (size_t i = 0; i < copies.size(); ++i) {  // round-robin: copy i on stream i % (1 + nside)
+      const int k = (int)(i % (size_t)(1 + nside));
+      const auto& d = copies[i];
+      PDCC_HIP(hipMemcpyAsync(d.dst, d.src, d.bytes, hipMemcpyDeviceToDevice, k == 0 ? s : ds.sdma_side[k - 1]));
+    }
+    for (int k = 0; k < nside; ++k) {
+      hipEvent_t join = ds.events->get();
+      PDCC_HIP(hipEventRecord(join, ds.sdma_side[k]));
+      PDCC_HIP(hipStreamWaitEvent(s, join, 0));
+      ds.events->put(join);
+    }
+  }
+  ic.launch(bar, s);  // departure
+  ic.zc_note_launch(ic.new_launch_event(s));  // (the mappings stay open until the pulls are done)
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  sdma_ran_ = true;
+  return true;
 }
 
 c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& ds,
@@ -232,7 +316,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_run(Coll c, DeviceState& 
     // an async collective (comm stream) runs next to the caller's compute: its IPC launches
     // take at most PDCC_IPC_ASYNC_GRID workgroups (async_op=True only: PDCC_STREAM=comm puts
     // synchronous calls on the comm stream too, and those keep the full grid)
-    IpcComm::AsyncScope as(ipcp.get(), op_async_ && comm != cur && !stream);
+    IpcComm::AsyncScope as(ipcp.get(), !stream && runs_capped(ds.device));  // (the autotuner keys on the same)
     fn(comm.stream());
   }
   if (rx && roctx_pop_) roctx_pop_();
@@ -290,6 +374,10 @@ void ProcessGroupMI355X::order_after_async(DeviceState& ds, hipStream_t s) {
   }
 }
 
+bool ProcessGroupMI355X::runs_capped(int device) const {
+  return op_async_ && cfg_.ipc_async_grid > 0 && cfg_.stream_mode != 3 && !capturing_on(device);
+}
+
 c10d::OpType ProcessGroupMI355X::op_type(Coll c) {
   switch (c) {
     case Coll::ALLREDUCE: return c10d::OpType::ALLREDUCE;
@@ -313,6 +401,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_issue(Coll c, DeviceState
                                                              std::function<void(hipStream_t)> job,
                                                              std::shared_ptr<IpcComm> ipcp) {
   hp_.lap(HostStage::CHOOSE);
+  {  // (zero-copy attempts of the autotuner's scratch runs do not label this call)
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    zc_parts_.clear();
+    sdma_ran_ = false;
+  }
   auto w = gpu_run(c, ds, keep_alive, std::move(outputs), timeout, [&](hipStream_t s) {
     hp_.lap(HostStage::PRE);
     job(s);
@@ -374,6 +467,14 @@ void ProcessGroupMI355X::enqueue_broadcast(Algo a, const at::Tensor& w, int root
                                            std::chrono::milliseconds to) {
   const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = w.nbytes();
+  if (a == Algo::IPC_SDMA && bytes >= cfg_.ipc_zc_min) {  // every non-root pulls the root's tensor
+    const bool is_root = rank_ == root;
+    if (sdma_run(ds, is_root ? w.data_ptr() : nullptr, is_root ? bytes : 0, s,
+                 [&](const std::vector<char*>& p, std::vector<kern::CopyDesc>& d) {
+                   if (!is_root) d.push_back({p[root], w.data_ptr(), bytes});
+                 }))
+      return;
+  }
   if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -411,6 +512,16 @@ void ProcessGroupMI355X::enqueue_allgather(Algo a, const at::Tensor& wi, const s
   const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = wi.nbytes();
   const bool receiver = !rooted || rank_ == root;
+  if (a == Algo::IPC_SDMA && bytes >= cfg_.ipc_zc_min) {  // every receiver pulls each rank's input
+    if (sdma_run(ds, wi.data_ptr(), bytes, s, [&](const std::vector<char*>& p, std::vector<kern::CopyDesc>& d) {
+          if (!receiver) return;
+          for (int k = 1; k <= size_; ++k) {  // peers rotated from this rank: the first pulls spread over links
+            const int r = (rank_ + k) % size_;
+            d.push_back({r == rank_ ? wi.data_ptr() : p[r], wo[r].data_ptr(), bytes});
+          }
+        }))
+      return;
+  }
   if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -477,6 +588,16 @@ void ProcessGroupMI355X::enqueue_scatter(Algo a, const std::vector<at::Tensor>& 
                                          DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
   const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
   const size_t bytes = wo.nbytes();
+  if (a == Algo::IPC_SDMA && bytes >= cfg_.ipc_zc_min) {
+    // every rank pulls its chunk from the root's flat list (a list that is not one buffer is not
+    // exportable: the record says so on every rank and the IPC kernels run instead)
+    const bool is_root = rank_ == root;
+    const void* z = is_root ? (is_flat(wi, bytes) ? wi[0].data_ptr() : nullptr) : nullptr;
+    if (sdma_run(ds, z, is_root ? bytes * size_ : 0, s, [&](const std::vector<char*>& p, std::vector<kern::CopyDesc>& d) {
+          d.push_back({is_root ? wi[root].data_ptr() : p[root] + (size_t)rank_ * bytes, wo.data_ptr(), bytes});
+        }))
+      return;
+  }
   if (is_ipc(a)) {
     IpcComm& ic = ipc(ds);
     kern::IpcCall c{};
@@ -586,6 +707,18 @@ void ProcessGroupMI355X::enqueue_reduce_scatter(Algo a, const std::vector<at::Te
 void ProcessGroupMI355X::enqueue_alltoall(Algo a, const std::vector<at::Tensor>& wi, const std::vector<at::Tensor>& wo,
                                           bool equal, DeviceState& ds, hipStream_t s, std::chrono::milliseconds to) {
   const StagedOnly staged_only(staged_only_, a == Algo::IPC_STAGED);  // (read by ipc_run)
+  if (a == Algo::IPC_SDMA && equal && wi[0].nbytes() >= cfg_.ipc_zc_min) {
+    // rank r pulls block r of every rank's flat input into its out[q] (a non-flat input: the IPC kernels)
+    const size_t chunk = wi[0].nbytes();
+    const void* z = is_flat(wi, chunk) ? wi[0].data_ptr() : nullptr;
+    if (sdma_run(ds, z, chunk * size_, s, [&](const std::vector<char*>& p, std::vector<kern::CopyDesc>& d) {
+          for (int k = 1; k <= size_; ++k) {
+            const int q = (rank_ + k) % size_;
+            d.push_back({q == rank_ ? wi[rank_].data_ptr() : p[q] + (size_t)rank_ * chunk, wo[q].data_ptr(), chunk});
+          }
+        }))
+      return;
+  }
   if (is_ipc(a)) {
     TORCH_CHECK(equal, "pdcc: the IPC all-to-all needs equal splits");
     IpcComm& ic = ipc(ds);

@@ -126,28 +126,36 @@ void ProcessGroupMI355X::init_topology(DeviceState& ds) {
   // every rank): a rank started with different PDCC_IPC_GRID / _WIDE_GRID / _ASYNC_GRID settings is
   // brought to the group's minimum instead of hanging its peers' barriers. PDCC_IPC_DYN likewise: it
   // sets the dynamic all-reduce's chunk size (every rank must number the chunks alike) and whether the
-  // autotuner races it (every rank must race the same candidates).
+  // autotuner races it (every rank must race the same candidates). The zero-copy size guard too: a
+  // guarded rank must never import a record a rank without the guard exported (the stall the guard
+  // exists to prevent), so it is lifted only if every rank lifts it (slot 5: 1 = lifted, min-voted).
   {
-    const int32_t mine3[5] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid, cfg_.ipc_dyn,
-                              cfg_.ipc_dyn_min_rows};
+    constexpr int kN = 6;
+    const int32_t mine3[kN] = {cfg_.ipc_grid, cfg_.ipc_wide_grid, cfg_.ipc_async_grid, cfg_.ipc_dyn,
+                               cfg_.ipc_dyn_min_rows, cfg_.ipc_zc_size_guard ? 0 : 1};
     const auto gv = store_allgather(store_, "pdcc/dev_grids", rank_, size_,
                                     std::vector<uint8_t>(reinterpret_cast<const uint8_t*>(mine3),
                                                          reinterpret_cast<const uint8_t*>(mine3) + sizeof(mine3)));
-    int32_t lo[5] = {mine3[0], mine3[1], mine3[2], mine3[3], mine3[4]};
+    int32_t lo[kN];
+    std::memcpy(lo, mine3, sizeof(lo));
     for (const auto& v : gv) {
-      if (v.size() != sizeof(mine3)) continue;
-      int32_t t[5];
+      TORCH_CHECK(v.size() == sizeof(mine3), "pdcc: malformed IPC settings vote");
+      int32_t t[kN];
       std::memcpy(t, v.data(), sizeof(t));
-      for (int k = 0; k < 5; ++k) lo[k] = std::min(lo[k], t[k]);
+      for (int k = 0; k < kN; ++k) lo[k] = std::min(lo[k], t[k]);
     }
     if (std::memcmp(lo, mine3, sizeof(lo)) != 0)
-      fprintf(stderr, "[pdcc r%d] IPC grid caps / PDCC_IPC_DYN / _DYN_MIN_ROWS differ between ranks: using the group "
-              "minimum %d/%d/%d/%d/%d\n", rank_, lo[0], lo[1], lo[2], lo[3], lo[4]);
+      fprintf(stderr, "[pdcc r%d] IPC grid caps / PDCC_IPC_DYN / _DYN_MIN_ROWS / _ZC_SIZE_GUARD differ between ranks: "
+              "using the group minimum %d/%d/%d/%d/%d, size guard %s\n", rank_, lo[0], lo[1], lo[2], lo[3], lo[4],
+              lo[5] ? "lifted" : "on");
     cfg_.ipc_grid = std::max(1, lo[0]);
     cfg_.ipc_wide_grid = lo[1];
     cfg_.ipc_async_grid = lo[2];
     cfg_.ipc_dyn = lo[3];
     cfg_.ipc_dyn_min_rows = lo[4];
+    cfg_.ipc_zc_size_guard = lo[5] == 0;
+    // (as Config::from_env does for a guarded rank: its own staging window must not need the guard)
+    if (cfg_.ipc_zc_size_guard && cfg_.ipc_max_staging >= (size_t{1} << 31)) cfg_.ipc_max_staging = size_t{1} << 30;
   }
   ds.recs = recs;
   ds.shared_device = shared;

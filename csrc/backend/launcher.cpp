@@ -99,19 +99,15 @@ host::ShmComm& ProcessGroupMI355X::exchange_channel(DeviceState& ds) {
 // so that the staged fallback of each fits a staging window of at most kGateChunk.
 constexpr size_t kGateChunk = 256u << 20;
 
-void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen,
-                                   size_t unit, size_t body, size_t per_call_max, hipStream_t s) {
+uint64_t ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, const void* zbuf, size_t zlen,
+                                       size_t unit, size_t body, size_t per_call_max, hipStream_t s) {
   IpcComm& ic = ipc(ds);
   hp_.lap(HostStage::ENQUEUE);
   const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, false);
   hp_.lap(HostStage::ZC_EXPORT);
   const uint64_t t = ic.gate_reserve();
   hp_.lap(HostStage::ZC_RESERVE);
-  static const size_t gate_chunk = [] {  // PDCC_TEST_GATE_CHUNK: A/B hook (same value on every rank)
-    const char* e = std::getenv("PDCC_TEST_GATE_CHUNK");
-    return e ? std::max<size_t>(size_t{1} << 20, std::strtoull(e, nullptr, 0)) : kGateChunk;
-  }();
-  size_t chunk = std::min(per_call_max, gate_chunk) / unit * unit;
+  size_t chunk = std::min(per_call_max, kGateChunk) / unit * unit;
   if (chunk == 0) chunk = unit;
   for (size_t off = 0; off < body; off += chunk) {
     kern::IpcCall c = call;
@@ -172,6 +168,16 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
       std::lock_guard<std::mutex> lk2(dsp->launcher->mu);
       ++dsp->launcher->fallbacks;  // a rank could not export / map: this call runs staged
     }
+    {  // the call's engine label (record()) is settled from this, not from the intent
+      IpcLauncher& L2 = *dsp->launcher;
+      std::lock_guard<std::mutex> lk2(L2.mu);
+      if (L2.outcome.size() >= 4096)  // abandoned tickets (autotune races' scratch calls): keep it bounded
+        for (auto it = L2.outcome.begin(); it != L2.outcome.end();)
+          it = it->first + 2048 < t ? L2.outcome.erase(it) : std::next(it);
+      L2.outcome[t] = ok;
+      L2.done_hi = std::max(L2.done_hi, t);
+    }
+    dsp->launcher->outcome_cv.notify_all();
     icp->gate_publish(t, ok, ptrs);
     const auto t_end = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> lk3(dsp->launcher->mu);
@@ -182,6 +188,7 @@ void ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& call, c
   L.pushed.fetch_add(1, std::memory_order_release);
   L.cv.notify_one();
   hp_.lap(HostStage::ZC_JOB);
+  return t;
 }
 
 void ProcessGroupMI355X::stop_launchers() {

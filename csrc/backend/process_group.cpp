@@ -553,24 +553,109 @@ void ProcessGroupMI355X::record_setup(const std::string& key, std::chrono::stead
 void ProcessGroupMI355X::record(Coll c, const char* algo, size_t bytes, std::chrono::steady_clock::time_point t0) {
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   std::lock_guard<std::mutex> lk(stats_mu_);
-  // an IPC op whose body ran zero-copy (ipc_run) is counted as "<algo>_zc"
-  const std::string name = std::string(algo) + (zc_ran_ && std::strncmp(algo, "ipc", 3) == 0 ? "_zc" : "");
-  zc_ran_ = false;
-  const std::string key = std::string(coll_name(c)) + "/" + name;
-  OpStats& s = stats_[key];
-  s.calls++;
-  s.bytes += bytes;
-  s.host_ms += ms;
-  last_algo_ = name;
+  if (sdma_ran_) algo = "ipc_sdma";  // (the engine job ran on the copy engines: sdma_run)
+  sdma_ran_ = false;
+  PendingRec p{++rec_id_, c, algo, bytes, ms, {}};
+  // an IPC op whose zero-copy attempts all ran zero-copy is counted as "<algo>_zc" -- decided from
+  // the outcome (a gated attempt's exchange may still be running: the record waits in pending_)
+  if (std::strncmp(algo, "ipc", 3) == 0) p.parts = std::move(zc_parts_);
+  zc_parts_.clear();
   if (fr_cap_ > 0) {
-    FrEntry e{op_seq_.load(), key, bytes,
+    FrEntry e{op_seq_.load(), std::string(coll_name(c)) + "/" + algo + (p.parts.empty() ? "" : "_zc?"), bytes,
               std::chrono::duration<double, std::milli>(t0 - created_).count(), (bool)fr_last_work_,
               fr_last_work_ ? c10::weak_intrusive_ptr<WorkMI355X>(fr_last_work_)
-                            : c10::weak_intrusive_ptr<WorkMI355X>(c10::intrusive_ptr<WorkMI355X>())};
+                            : c10::weak_intrusive_ptr<WorkMI355X>(c10::intrusive_ptr<WorkMI355X>()),
+              p.id};
     fr_last_work_.reset();
     fr_.push_back(std::move(e));
     while (fr_.size() > fr_cap_) fr_.pop_front();
   }
+  pending_.push_back(std::move(p));
+  zc_resolve_locked(false);
+}
+
+void ProcessGroupMI355X::finalize_locked(PendingRec& p) {
+  bool zc = !p.parts.empty();
+  for (const auto& z : p.parts) zc = zc && z.state == 1;
+  if (!p.parts.empty()) ++(zc ? zc_ran_calls_ : zc_staged_calls_);
+  const std::string name = p.algo + (zc ? "_zc" : "");
+  const std::string key = std::string(coll_name(p.coll)) + "/" + name;
+  OpStats& s = stats_[key];
+  s.calls++;
+  s.bytes += p.bytes;
+  s.host_ms += p.ms;
+  if (p.id == rec_id_) last_algo_ = name;
+  if (!p.parts.empty())
+    for (auto it = fr_.rbegin(); it != fr_.rend(); ++it)
+      if (it->rec_id == p.id) {
+        it->what = key;
+        break;
+      }
+}
+
+void ProcessGroupMI355X::zc_resolve_locked(bool block) {
+  const auto deadline = std::chrono::steady_clock::now() + timeout_;
+  while (!pending_.empty()) {
+    PendingRec& p = pending_.front();
+    bool done = true;
+    for (auto& z : p.parts) {
+      if (z.state >= 0) continue;
+      IpcLauncher& L = *z.launcher;
+      std::unique_lock<std::mutex> lk(L.mu);
+      for (;;) {
+        auto it = L.outcome.find(z.ticket);
+        if (it != L.outcome.end()) {
+          z.state = it->second ? 1 : 0;
+          L.outcome.erase(it);
+          break;
+        }
+        // (its job has run but the entry is gone, or the exchange can no longer run: not zero-copy)
+        if (L.done_hi >= z.ticket || L.stop || health_->poisoned.load() || !block ||
+            std::chrono::steady_clock::now() >= deadline) {
+          if (block || L.done_hi >= z.ticket || L.stop) z.state = 0;
+          break;
+        }
+        L.outcome_cv.wait_for(lk, std::chrono::milliseconds(50));
+      }
+      done = done && z.state >= 0;
+    }
+    if (!done) break;  // (records settle in issue order: their jobs run in that order)
+    finalize_locked(p);
+    pending_.pop_front();
+  }
+}
+
+std::string ProcessGroupMI355X::last_algo() {
+  std::lock_guard<std::mutex> lk(stats_mu_);
+  zc_resolve_locked(true);
+  return last_algo_;
+}
+
+std::map<std::string, uint64_t> ProcessGroupMI355X::zc_counters() {
+  std::map<std::string, uint64_t> out;
+  {
+    std::lock_guard<std::mutex> lk(stats_mu_);
+    zc_resolve_locked(true);
+    out["zc_calls"] = zc_ran_calls_;
+    out["zc_fallbacks"] = zc_staged_calls_;
+    out["zc_pending"] = pending_.size();
+  }
+  uint64_t size_ref = 0, full_ref = 0, xchg_fallbacks = 0;
+  std::lock_guard<std::mutex> lk(init_mu_);
+  for (auto& kv : devs_) {
+    if (kv.second->ipc) {
+      size_ref += kv.second->ipc->zc_size_refusals();
+      full_ref += kv.second->ipc->zc_full_refusals();
+    }
+    if (kv.second->launcher) {
+      std::lock_guard<std::mutex> l2(kv.second->launcher->mu);
+      xchg_fallbacks += kv.second->launcher->fallbacks;
+    }
+  }
+  out["zc_size_refusals"] = size_ref;
+  out["zc_full_refusals"] = full_ref;
+  out["zc_exchange_fallbacks"] = xchg_fallbacks;
+  return out;
 }
 
 std::vector<std::tuple<std::string, uint64_t, double>> ProcessGroupMI355X::host_profile() {
@@ -584,6 +669,7 @@ std::vector<std::tuple<std::string, uint64_t, double>> ProcessGroupMI355X::host_
 
 std::vector<ProcessGroupMI355X::FrRecord> ProcessGroupMI355X::flight_recorder() {
   std::lock_guard<std::mutex> lk(stats_mu_);
+  zc_resolve_locked(false);  // (never waits: also read while a peer is stuck)
   std::vector<FrRecord> out;
   for (auto& e : fr_) {
     std::string st = "done";
@@ -611,10 +697,12 @@ std::string ProcessGroupMI355X::flight_recorder_dump(size_t last) {
 
 std::map<std::string, OpStats> ProcessGroupMI355X::stats() {
   std::lock_guard<std::mutex> lk(stats_mu_);
+  zc_resolve_locked(true);
   return stats_;
 }
 void ProcessGroupMI355X::reset_stats() {
   std::lock_guard<std::mutex> lk(stats_mu_);
+  zc_resolve_locked(true);  // (a call issued before the reset is not counted after it)
   stats_.clear();
 }
 
@@ -744,7 +832,8 @@ void ProcessGroupMI355X::set_algo(const std::string& a) {
   else if (a == "ipc_wide") cfg_.force_algo = Algo::IPC_WIDE;
   else if (a == "ipc_staged") cfg_.force_algo = Algo::IPC_STAGED;
   else if (a == "ipc_dyn") cfg_.force_algo = Algo::IPC_DYN;
-  else TORCH_CHECK(false, "set_algo: expected auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|host, got ", a);
+  else if (a == "ipc_sdma") cfg_.force_algo = Algo::IPC_SDMA;
+  else TORCH_CHECK(false, "set_algo: expected auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|ipc_sdma|host, got ", a);
 }
 
 void ProcessGroupMI355X::set_ipc_thresholds(int64_t one_shot_max, int64_t two_shot_max, int64_t copy_max) {

@@ -141,8 +141,13 @@ PYBIND11_MODULE(_C, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("stats",
            [](pdcc::ProcessGroupMI355X& pg) {
+             std::map<std::string, pdcc::OpStats> st;
+             {  // (may wait for pending zero-copy outcomes)
+               py::gil_scoped_release nogil;
+               st = pg.stats();
+             }
              py::dict d;
-             for (const auto& kv : pg.stats())
+             for (const auto& kv : st)
                d[py::str(kv.first)] = py::make_tuple(kv.second.calls, kv.second.bytes, kv.second.host_ms);
              return d;
            })
@@ -161,6 +166,7 @@ PYBIND11_MODULE(_C, m) {
                d["ipc_us"] = r.ipc_us;
                d["push_us"] = r.push_us;
                d["dyn_us"] = r.dyn_us;
+               d["sdma_us"] = r.sdma_us;
                d["wide_us"] = r.wide_us;
                d["ipc_wide_us"] = r.ipc_wide_us;
                d["staged_us"] = r.staged_us;
@@ -190,7 +196,8 @@ PYBIND11_MODULE(_C, m) {
       .def("reset_stats", &pdcc::ProcessGroupMI355X::reset_stats)
       .def("describe", &pdcc::ProcessGroupMI355X::describe)
       .def("timeout_ms", &pdcc::ProcessGroupMI355X::timeout_ms)
-      .def("last_algo", &pdcc::ProcessGroupMI355X::last_algo)
+      .def("last_algo", &pdcc::ProcessGroupMI355X::last_algo, py::call_guard<py::gil_scoped_release>())
+      .def("zc_counters", &pdcc::ProcessGroupMI355X::zc_counters, py::call_guard<py::gil_scoped_release>())
       .def("healthy", &pdcc::ProcessGroupMI355X::healthy)
       .def("health_message", &pdcc::ProcessGroupMI355X::health_message)
       .def("set_algo", &pdcc::ProcessGroupMI355X::set_algo)

@@ -115,11 +115,8 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
-  if (const char* tf = std::getenv("PDCC_TEST_IPC_FLAGS")) test_flags_ = std::atoi(tf);
   shared_grid_ = std::max(1, 256 / std::max(1, world));
   shared_wide_grid_ = std::max(1, kSharedWideSlots / std::max(1, world) - 1);
-  if (const char* sg = std::getenv("PDCC_TEST_SHARED_GRID"))  // A/B hook (same value on every rank): one cap
-    shared_grid_ = shared_wide_grid_ = std::max(1, std::min(512 / std::max(1, world) - 1, std::atoi(sg)));
   zc_cache_ = std::max<size_t>(zc_cache, 1);
   closing_limit_ = std::max<size_t>(2, (size_t)kern::kZcTab > zc_cache_ ? (size_t)kern::kZcTab - zc_cache_ : 0);
   if (world < 2 || world > kern::kMaxRanks)
@@ -335,7 +332,6 @@ kern::IpcView IpcComm::view(const std::vector<char*>& bufs) const {
 
 void IpcComm::launch_view(const kern::IpcView& v, kern::IpcCall call, hipStream_t stream) {
   ++seq_;  // launches so far (informational: the kernels keep their own per-block call counters)
-  call.test_flags = test_flags_;
   if (shared_device_) {
     // All ranks' grids run on ONE device (test setups, rehearsals): small calls at 256 / W workgroups per
     // rank; from kSharedWideMin bytes per launch W x (cap + exchange block) = kSharedWideSlots in all, within

@@ -309,7 +309,6 @@ class IpcComm {
   uint64_t* trace_host_ = nullptr;        // PDCC_IPC_TRACE ring (pinned, device-visible), or null
   uint64_t* trace_dev_ = nullptr;
   uint32_t trace_cap_ = 0;
-  int test_flags_ = 0;  // PDCC_TEST_IPC_FLAGS (measurement hook, kern::IpcCall::test_flags)
 
   char* my_staging_ = nullptr;
   size_t cap_ = 0;                         // staging bytes

@@ -34,7 +34,9 @@ ncclConfig_t make_config(const RcclOpts& o, bool for_split) {
   if (o.max_ctas > 0) cfg.maxCTAs = o.max_ctas;
   // RCCL validates the pair as given: a floor with the ceiling left undefined is rejected
   // ("Invalid config min/max channels attribute value 28/-2147483648", found by the world-1 RCCL
-  // rehearsal of bench.py's CTA sweep): a floor alone means exactly that many channels
+  // rehearsal of bench.py's CTA sweep). RCCL's channel maximum is not part of its public API, so a
+  // floor alone (PDCC_RCCL_MIN_CTAS without _MAX_CTAS) means exactly that many channels; bench.py's
+  // sweep sets both and reports exact counts
   if (o.min_ctas > 0 && cfg.maxCTAs < o.min_ctas) cfg.maxCTAs = o.min_ctas;
   if (for_split) cfg.splitShare = o.split_share ? 1 : 0;
   return cfg;

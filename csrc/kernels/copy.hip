@@ -73,13 +73,13 @@ __device__ __forceinline__ void ipc_allgather_dyn(const DView& v, const DCall& c
   const size_t nt = c.bytes / kTile;
   const uint32_t K = kern::dyn_rows_per_chunk(nt, G, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
-  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
-  dyn_claim_loop(v, nc, c.test_flags, tr, b, G, [&](uint32_t it) {
+  const uint32_t dep = dyn_epoch(v, tr);
+  dyn_claim_loop(v, nc, tr, b, G, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const PeerTileMap<W> m{&v, &c, 0, c.bytes, (uint32_t)(v.rank + it), t0, 1, t1};
     ipc_pipe<DType::U8, RedOp::COPY, 1, kCopyDepth>(lds, m, 1);
   });
-  dyn_depart(v, dep, true, c.test_flags, tr, G);
+  dyn_depart(v, dep, true, tr, G);
 }
 
 // Zero-copy copies (IpcCall::zc): peers' user buffers are read in place; data
@@ -141,10 +141,9 @@ __device__ __forceinline__ void ipc_copy_zc(const DView& v, const DCall& c, char
 
 template <int W>
 __device__ __forceinline__ void ipc_copy_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
-                                              uint32_t seq0, bool early) {
+                                              uint32_t seq) {
   const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
-  const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
   if (c.coll == IpcColl::BARRIER) {  // the arrival barrier is the whole collective
@@ -238,11 +237,10 @@ __global__ void __launch_bounds__(256) k_ipc_copy(IpcView v, IpcCall c) {
     zx_publish_verdict(c);
     return;
   }
-  const bool early = (c.test_flags & 32) == 0;  // (see k_ipc_reduce)
-  const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
+  const uint32_t seq = block_seq(v, block_seq_load(v));  // (see k_ipc_reduce)
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_copy_body<W>(sv, sc, lds, tr, seq0, early);
+  ipc_copy_body<W>(sv, sc, lds, tr, seq);
   tr.finish(v);
 }
 

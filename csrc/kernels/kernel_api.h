@@ -243,7 +243,7 @@ constexpr size_t kZxBytes = 1024 + kGateSlots * sizeof(GateSlot);
 // ready word per chunk. Words hold a per-rank dyn-call epoch (never 0), compared for equality.
 constexpr size_t kDynOffset = kZxOffset + kZxBytes;
 // (u32 word indices from kDynOffset; the two counters every block hits sit 128 B apart)
-constexpr size_t kDynCtlBytes = 512;  // IpcView::dctl (and the round-4 copy at kDynOffset)
+constexpr size_t kDynCtlBytes = 512;  // IpcView::dctl
 constexpr int kDynEpochWord = 0;   // epoch of this rank's last finished dyn call
 constexpr int kDynClaimWord = 32;  // work-item counter of the running call (reset by its last block)
 constexpr int kDynExitWord = 64;   // blocks of the running call that finished (reset by the last one)
@@ -300,11 +300,6 @@ struct IpcCallT {
   int dyn;  // > 0: a zero-copy ALLREDUCE_2SHOT runs the dynamic protocol with about `dyn` chunks per
             // workgroup (see kDynOffset); staged runs ignore it
   int dyn_min_rows;  // rows per dynamic-protocol item, at least (0 = kDynMinRows; group-wide setting)
-  int test_flags;  // PDCC_TEST_IPC_FLAGS, measurements only: bit 0 = the zero-copy reductions' arrival
-                   // barrier without its release / acquire (what the data hand-over costs); bits 1-2:
-                   // reduce_impl.h zc pipes; bit 3 = dyn claims from the first item (round-4 claim
-                   // loop); bit 4 = dyn control words in the uncached signal area (round-4 placement); bit 5 =
-                   // the call number taken after the arguments are staged (round-4 order)
 };
 using IpcCall = IpcCallT<RawPtr>;
 

@@ -185,9 +185,8 @@ struct OneSrcMap {  // copy tile t from one buffer to another
 
 constexpr int kCopyDepth = 4;
 
-// The zero-copy all-reduce's pipes. PDCC_TEST_IPC_FLAGS (IpcCall::test_flags, A/B measurements only):
-// bit 1 = non-temporal loads and stores in the gather phase (tiles read once, written once), bit 2 =
-// non-temporal stores in the reduce phase.
+// The zero-copy all-reduce's pipes (non-temporal loads / stores in either phase measured as noise,
+// profiles/r5/nt_and_dyn_items_ab.jsonl: plain cached pipes).
 // The gather phase runs in the reduce kernels, whose LDS is sized for the reduce pipe (W x
 // DepthFor<W> tiles, >= 32 KiB for every W): the copy keeps 8 tiles in flight instead of 4 there
 // (Little's law: the bytes in flight per workgroup set a streaming copy's rate).
@@ -196,14 +195,12 @@ static_assert(2 * DepthFor<2>::value >= kZcCopyDepth && 3 * DepthFor<3>::value >
                   5 * DepthFor<5>::value >= kZcCopyDepth,
               "the reduce kernels' LDS must hold the gather phase's ring");
 template <class Map>
-__device__ __forceinline__ void zc_copy_pipe(char* lds, const Map& m, int flags) {
-  if (flags & 2) pipe_run<DType::U8, RedOp::COPY, 1, kZcCopyDepth, Map, 1, true, true>(lds, m, 1);
-  else ipc_pipe<DType::U8, RedOp::COPY, 1, kZcCopyDepth>(lds, m, 1);
+__device__ __forceinline__ void zc_copy_pipe(char* lds, const Map& m) {
+  ipc_pipe<DType::U8, RedOp::COPY, 1, kZcCopyDepth>(lds, m, 1);
 }
 template <DType DT, RedOp OP, int NSRC, int DEPTH, class Map>
-__device__ __forceinline__ void zc_reduce_pipe(char* lds, const Map& m, int avg_div, int flags) {
-  if (flags & 4) pipe_run<DT, OP, NSRC, DEPTH, Map, 1, true, PDCC_IPC_ZC_NTL != 0>(lds, m, avg_div);
-  else ipc_pipe_once<DT, OP, NSRC, DEPTH>(lds, m, avg_div);
+__device__ __forceinline__ void zc_reduce_pipe(char* lds, const Map& m, int avg_div) {
+  ipc_pipe_once<DT, OP, NSRC, DEPTH>(lds, m, avg_div);
 }
 
 // Owner-interleaved maps. A block's pipeline keeps DEPTH tiles in flight; if all
@@ -386,19 +383,16 @@ __device__ __forceinline__ bool dyn_wait(const DView& v, const uint32_t* w, uint
 // positions I write in phase 2 (tile q + W*r of MY tensor) were read by q in its phase 1 of
 // chunk c, which q finished before publishing ready[c]; my own tiles are written in phase 1
 // only, and peers read them after my ready word.
-// This rank's control words (claim / exit counters, epoch): ordinary device memory (IpcView::dctl),
-// or -- PDCC_TEST_IPC_FLAGS bit 4, A/B only -- the round-4 copy in the uncached signal area.
-__device__ __forceinline__ uint32_t* dyn_ctl(const DView& v, int flags) {
-  return (flags & 16) ? dyn_words(v, v.rank, kern::kDynOffset) : (uint32_t*)v.dctl;
-}
+// This rank's control words (claim / exit counters, epoch): ordinary device memory (IpcView::dctl).
+__device__ __forceinline__ uint32_t* dyn_ctl(const DView& v) { return (uint32_t*)v.dctl; }
 
 // This call's epoch: the previous dyn call's last block stored its own (never 0).
-__device__ __forceinline__ uint32_t dyn_epoch(const DView& v, int flags, const PhaseTrace* tr) {
+__device__ __forceinline__ uint32_t dyn_epoch(const DView& v, const PhaseTrace* tr) {
   __shared__ uint32_t s_dep;
   if (threadIdx.x == 0) {
     const uint64_t t0 = tr->now();
     const uint32_t e =
-        __hip_atomic_load(dyn_ctl(v, flags) + kern::kDynEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+        __hip_atomic_load(dyn_ctl(v) + kern::kDynEpochWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     s_dep = e ? e : 1u;
     tr->add(23, t0);
   }
@@ -414,16 +408,13 @@ __device__ __forceinline__ uint32_t dyn_epoch(const DView& v, int flags, const P
 // atomic's round trip overlaps the current item. Claims are monotonic (b < b + G < 2G <= 2G + k): a
 // block never holds an earlier item behind a later one, and a block's earlier items are always
 // smaller, so every phase-1 item (index < nc, waiting for nothing) is reached without a wait.
-// PDCC_TEST_IPC_FLAGS bit 3 (A/B only): the round-4 loop (item b, then G + the counter, claimed
-// from the first item on).
 // (b, G: this data block's index and the number of data blocks, see xchg_blocks)
 template <class Item>
-__device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, int flags, const PhaseTrace* tr,
-                                               uint32_t b, uint32_t G, Item&& item) {
+__device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, const PhaseTrace* tr, uint32_t b,
+                                               uint32_t G, Item&& item) {
   __shared__ uint32_t s_item;
-  uint32_t* const claim = dyn_ctl(v, flags) + kern::kDynClaimWord;
-  const bool old = (flags & 8) != 0;
-  const uint32_t base = old ? G : 2u * G;  // first claimed item
+  uint32_t* const claim = dyn_ctl(v) + kern::kDynClaimWord;
+  const uint32_t base = 2u * G;  // first claimed item
   uint32_t next = b;
   for (;;) {
     const uint64_t t0 = tr->now();
@@ -434,7 +425,7 @@ __device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, i
     if (threadIdx.x == 0) tr->add(16, t0);
     if (it >= total) break;
     if (threadIdx.x == 0) {
-      if (!old && it < G) next = it + G;  // the second static item
+      if (it < G) next = it + G;  // the second static item
       else next = total > base ? base + __hip_atomic_fetch_add(claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                : total;
       tr->count(20);
@@ -446,10 +437,9 @@ __device__ __forceinline__ void dyn_claim_loop(const DView& v, uint32_t total, i
 // Departure: once every block of mine is done (exit counter), the last one tells every peer, waits
 // until every peer's blocks are done too (nobody reads my tensor any more), then resets the counters
 // and publishes this call's epoch for the next dyn call.
-__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok, int flags, const PhaseTrace* tr,
-                                           uint32_t G) {
+__device__ __forceinline__ void dyn_depart(const DView& v, uint32_t dep, bool ok, const PhaseTrace* tr, uint32_t G) {
   const int me = v.rank, W = v.world;
-  uint32_t* const ctl = dyn_ctl(v, flags);
+  uint32_t* const ctl = dyn_ctl(v);
   const uint64_t t0 = tr->now();
   drain_vm();
   __syncthreads();
@@ -481,13 +471,13 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
   const uint32_t nc = (uint32_t)((nrows + K - 1) / K);
   uint32_t* const ready = dyn_words(v, me, kern::kDynReadyOffset);
   __shared__ uint32_t s_ok;
-  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
+  const uint32_t dep = dyn_epoch(v, tr);
   bool ok = true;
-  dyn_claim_loop(v, nc * W, c.test_flags, tr, b, G, [&](uint32_t it) {
+  dyn_claim_loop(v, nc * W, tr, b, G, [&](uint32_t it) {
     if (it < nc) {
       const size_t r0 = (size_t)it * K, r1 = r0 + K < nrows ? r0 + K : nrows;
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * r0, W, W * r1};
-      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div, c.test_flags);
+      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div);
       const uint64_t t0 = tr->now();
       drain_vm();  // every wave's stores and loads (a peer overwrites what I read once it sees ready)
       __syncthreads();
@@ -514,11 +504,11 @@ __device__ __forceinline__ void ipc_allreduce_dyn(const DView& v, const DCall& c
       if (ok) {
         const size_t r0 = (size_t)cc * K, r1 = r0 + K < nrows ? r0 + K : nrows;
         const OneSrcMap m{v.buf[q], v.buf[me], c.bytes, (size_t)q + W * r0, W, W * r1};
-        zc_copy_pipe(lds, m, c.test_flags);
+        zc_copy_pipe(lds, m);
       }
     }
   });
-  dyn_depart(v, dep, ok, c.test_flags, tr, G);
+  dyn_depart(v, dep, ok, tr, G);
 }
 
 // Dynamic zero-copy reduce-scatter (IpcCall::dyn): my output chunk in items of K tiles, each reduced
@@ -532,13 +522,13 @@ __device__ __forceinline__ void ipc_reduce_scatter_dyn(const DView& v, const DCa
   const size_t nt = c.bytes / kTile;
   const uint32_t K = kern::dyn_rows_per_chunk(nt, G, (uint32_t)c.dyn, (uint32_t)c.dyn_min_rows);
   const uint32_t nc = (uint32_t)((nt + K - 1) / K);
-  const uint32_t dep = dyn_epoch(v, c.test_flags, tr);
-  dyn_claim_loop(v, nc, c.test_flags, tr, b, G, [&](uint32_t it) {
+  const uint32_t dep = dyn_epoch(v, tr);
+  dyn_claim_loop(v, nc, tr, b, G, [&](uint32_t it) {
     const size_t t0 = (size_t)it * K, t1 = t0 + K < nt ? t0 + K : nt;
     const AllSrcMap<W> m{&v, (size_t)v.rank * c.zstride, (char*)c.out[0], c.bytes, t0, 1, t1};
     ipc_pipe_once<DT, OP, W, D>(lds, m, c.avg_div);
   });
-  dyn_depart(v, dep, true, c.test_flags, tr, G);
+  dyn_depart(v, dep, true, tr, G);
 }
 
 // Zero-copy reductions (IpcCall::zc): every rank's user buffer is read in place.
@@ -554,8 +544,7 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
   const size_t nt = c.bytes / kTile;
-  if (c.test_flags & 1) block_barrier<false>(v, ep, &tr);  // (measurement hook, see IpcCall::test_flags)
-  else block_barrier(v, ep, &tr);
+  block_barrier(v, ep, &tr);
   tr.mark(2);
   tr.mark(4);
   if (c.coll == IpcColl::ALLREDUCE_2SHOT && c.dyn) {
@@ -571,14 +560,14 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
   if (c.coll == IpcColl::ALLREDUCE_2SHOT) {
     {  // phase 1: my owned tiles (t % W == me) from every rank's buffer, reduced in place
       const AllSrcMap<W> m{&v, 0, v.buf[me], c.bytes, (size_t)me + W * b, W * G, nt};
-      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div, c.test_flags);
+      zc_reduce_pipe<DT, OP, W, D>(lds, m, c.avg_div);
     }
     tr.mark(5);
     block_barrier(v, ep + 2u);
     tr.mark(6);
     {  // phase 2: the other owners' reduced tiles
       const PeerRowMap<W> m{&v, v.buf[me], (uint32_t)b, b, G, nt / W};
-      zc_copy_pipe(lds, m, c.test_flags);
+      zc_copy_pipe(lds, m);
     }
   } else if (c.coll == IpcColl::ALLREDUCE_PUSH) {
     // every remote access is a write (xGMI writes are posted; reads wait a round trip)
@@ -623,11 +612,10 @@ __device__ __forceinline__ void ipc_reduce_zc(const DView& v, const DCall& c, ch
 
 template <DType DT, RedOp OP, int W>
 __device__ __forceinline__ void ipc_reduce_body(const DView& v, const DCall& c, char* lds, const PhaseTrace tr,
-                                                uint32_t seq0, bool early) {
+                                                uint32_t seq) {
   constexpr int D = DepthFor<W>::value;
   const size_t G = gridDim.x - xchg_blocks(c), b = blockIdx.x - xchg_blocks(c);  // the data blocks
   const int me = v.rank;
-  const uint32_t seq = early ? seq0 : block_seq(v, seq0);
   tr.seq(seq);
   tr.mark(12);
   const uint32_t ep = seq * kern::kEpochsPerCall, ph0 = ep + 1u, ph1 = ep + 2u;
@@ -706,14 +694,11 @@ __global__ void __launch_bounds__(256) k_ipc_reduce(IpcView v, IpcCall c) {
     zx_publish_verdict(c);
     return;
   }
-  // The block's call number is taken at entry, before the arguments are staged (PDCC_TEST_IPC_FLAGS
-  // bit 5, A/B only: the round-4 order -- seq0 = the raw load, taken in the body; no measurable
-  // difference, profiles/r5/seq_early_ab.jsonl).
-  const bool early = (c.test_flags & 32) == 0;
-  const uint32_t seq0 = early ? block_seq(v, block_seq_load(v)) : block_seq_load(v);
+  // The block's call number is taken at entry, before the arguments are staged.
+  const uint32_t seq = block_seq(v, block_seq_load(v));
   stage_args(v, c, sv, sc, tr);  // (a gated zero-copy launch waits for its buffers here)
   if (c.gate) tr.mark(3);    // gate passed (zero-copy calls do not stage: [3] is free there)
-  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq0, early);
+  ipc_reduce_body<DT, OP, W>(sv, sc, lds, tr, seq);
   tr.finish(v);
 }
 

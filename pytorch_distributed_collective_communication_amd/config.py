@@ -6,7 +6,7 @@ group is constructed; :func:`current` shows what a new group would use and
 
 | variable | default | meaning |
 |---|---|---|
-| PDCC_ALGO | auto | force ``rccl`` / ``rccl_wide`` / ``ipc`` / ``ipc_push`` / ``ipc_wide`` / ``ipc_staged`` (IPC without zero copy) / ``ipc_dyn`` (dynamic zero-copy 2-shot all-reduce) / ``host`` for GPU tensors (preferred if feasible) |
+| PDCC_ALGO | auto | force ``rccl`` / ``rccl_wide`` / ``ipc`` / ``ipc_push`` / ``ipc_wide`` / ``ipc_staged`` (IPC without zero copy) / ``ipc_dyn`` (dynamic zero-copy 2-shot all-reduce) / ``ipc_sdma`` (copy collectives as copy-engine pulls between mapped user buffers) / ``host`` for GPU tensors (preferred if feasible) |
 | PDCC_IPC | 1 | enable the hipIpc peer-memory path |
 | PDCC_IPC_SELFTEST | 1 | run the IPC protocol once on known data when a group first uses a GPU; any failure on any rank disables IPC for that group |
 | PDCC_IPC_SELFTEST_MS | 20000 | spin timeout of the self-test's cross-GPU barriers (capped by the group timeout) |
@@ -23,6 +23,8 @@ group is constructed; :func:`current` shows what a new group would use and
 | PDCC_IPC_ZC_SIZE_GUARD | 1 | zero-copy refuses buffers whose allocation size has bit 31 set (2-4 GiB, 6-8 GiB: a peer's mapping of them stalls on this ROCm image); they run staged, and PDCC_IPC_MAX_STAGING stays below 2 GiB |
 | PDCC_IPC_ZX | 1 | gated zero-copy calls resolve the peers' buffers on the device (mapping table); every rank's setting is voted on (AND) at the group's first GPU use |
 | PDCC_IPC_DYN | 3 | chunks per workgroup of the dynamic zero-copy 2-shot all-reduce (``ipc_dyn``: workgroups claim chunks from a counter, per-chunk ready words instead of a block-pairwise barrier), which the autotuner races for zero-copy all_reduce keys; 0: not raced; agreed group-wide (minimum) |
+| PDCC_IPC_SDMA | 1 | the autotuner races the copy-engine engine (``ipc_sdma``: hipMemcpyAsync pulls between IPC-mapped user buffers, no CU kernel) for broadcast / all_gather / gather / scatter / all_to_all keys of zero-copy sizes |
+| PDCC_SDMA_STREAMS | 2 | side streams one ``ipc_sdma`` call's pulls fan out over (0..6) |
 | PDCC_IPC_DYN_MIN_ROWS | 0 (= 16) | rows (W tiles each) per item of the dynamic protocols, at least: every item is its own short pipeline, so small items make them latency-bound; agreed group-wide (minimum) |
 | PDCC_IPC_WIDE_GRID | 1024 | workgroup cap of the ``ipc_wide`` all-reduce the autotuner races for bulk keys on distinct GPUs (0: off) |
 | PDCC_AUTOTUNE | 1 | every GPU collective with two feasible engines: time both on the first call per (collective, dtype, op/layout, power-of-two size) key (IPC result checked against the reference engine's), adopt the faster on all ranks |
@@ -91,6 +93,8 @@ class Config:
     ipc_push: bool = True
     ipc_dyn: int = 3
     ipc_dyn_min_rows: int = 0
+    ipc_sdma: bool = True
+    sdma_streams: int = 2
     ipc_zc_min: int = 1 << 20
     ipc_ll_max: int = 256 << 10
     ipc_zc_cache: int = 16
@@ -138,7 +142,7 @@ _ENV = {
     "algo": "PDCC_ALGO", "ipc": "PDCC_IPC", "ipc_selftest": "PDCC_IPC_SELFTEST",
     "ipc_selftest_ms": "PDCC_IPC_SELFTEST_MS", "ipc_1shot_max": "PDCC_IPC_1SHOT_MAX",
     "ipc_2shot_max": "PDCC_IPC_2SHOT_MAX", "ipc_copy_max": "PDCC_IPC_COPY_MAX",
-    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_dyn": "PDCC_IPC_DYN", "ipc_dyn_min_rows": "PDCC_IPC_DYN_MIN_ROWS", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
+    "ipc_max_staging": "PDCC_IPC_MAX_STAGING", "ipc_zc": "PDCC_IPC_ZC", "ipc_push": "PDCC_IPC_PUSH", "ipc_dyn": "PDCC_IPC_DYN", "ipc_dyn_min_rows": "PDCC_IPC_DYN_MIN_ROWS", "ipc_sdma": "PDCC_IPC_SDMA", "sdma_streams": "PDCC_SDMA_STREAMS", "ipc_zc_min": "PDCC_IPC_ZC_MIN", "ipc_ll_max": "PDCC_IPC_LL_MAX",
     "ipc_zc_cache": "PDCC_IPC_ZC_CACHE", "ipc_zc_async": "PDCC_IPC_ZC_ASYNC",
     "ipc_zx": "PDCC_IPC_ZX", "ipc_zc_size_guard": "PDCC_IPC_ZC_SIZE_GUARD", "ipc_async_grid": "PDCC_IPC_ASYNC_GRID", "rccl_init_timeout_s": "PDCC_RCCL_INIT_TIMEOUT_S",
     "rccl_nonblocking": "PDCC_RCCL_NONBLOCKING", "autotune": "PDCC_AUTOTUNE",
@@ -173,8 +177,10 @@ def current(environ=None) -> Config:
         raw = env.get(_ENV[f.name])
         if raw not in (None, ""):
             setattr(c, f.name, _parse(f.type, raw))
-    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "ipc_wide", "ipc_staged", "ipc_dyn", "host"):
-        raise ValueError(f"PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|host, got {c.algo!r}")
+    if c.algo not in ("auto", "rccl", "rccl_wide", "ipc", "ipc_push", "ipc_wide", "ipc_staged", "ipc_dyn", "ipc_sdma",
+                      "host"):
+        raise ValueError("PDCC_ALGO must be auto|rccl|rccl_wide|ipc|ipc_push|ipc_wide|ipc_staged|ipc_dyn|ipc_sdma|host, "
+                         f"got {c.algo!r}")
     if c.stream not in ("auto", "high", "comm", "current"):
         raise ValueError(f"PDCC_STREAM must be auto|high|comm|current, got {c.stream!r}")
     if c.rccl_group_comm not in ("share", "split", "init"):

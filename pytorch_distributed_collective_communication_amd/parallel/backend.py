@@ -61,6 +61,14 @@ def _backend_options(backend):
 
 def _create(dist_opts, backend_opts):
     C = _native()
+    # an earlier RCCL environment sweep's verdict for this topology (utils/rccl_env.py), before the
+    # process's first RCCL communicator reads its environment
+    from ..utils import rccl_env
+
+    try:
+        rccl_env.apply_persisted(int(dist_opts.group_size))
+    except Exception:  # (a malformed file never stops a group from coming up)
+        pass
     return C.ProcessGroupMI355X(
         dist_opts.store,
         dist_opts.group_rank,
@@ -148,6 +156,12 @@ def stats(group=None) -> dict:
 
 def last_algo(group=None) -> str:
     return native_backend(group).last_algo()
+
+
+def zc_counters(group=None) -> dict:
+    """Zero-copy outcomes of the group's GPU calls: ``zc_calls`` (ran zero-copy), ``zc_fallbacks``
+    (attempted, ran staged), plus the export refusals (size guard, full mapping list)."""
+    return dict(native_backend(group, "cuda").zc_counters())
 
 
 def describe(group=None) -> str:

@@ -22,9 +22,18 @@ Two drivers share one child:
   backend forwards those to ``NCCL_*`` at its first communicator,
   csrc/device/rccl_comm.cpp ``forward_rccl_env``).
 
-Points: ``NCCL_BUFFSIZE`` in {RCCL default (4 MiB), 8, 16, 32 MiB} x ``NCCL_PROTO``
-in {RCCL default, Simple}, run in that order inside a wall-clock budget (a point
-that would start after the budget is recorded as skipped).
+Points (run in this order inside a wall-clock budget; a point that would start after the
+budget is recorded as skipped): RCCL's defaults; the algorithm forced to ``NCCL_ALGO=Ring``
+and ``Tree``; RCCL's MSCCL all-pairs algorithms (``RCCL_MSCCL_ENABLE``, the shipped
+``allreduce-allpairs-8n-*.xml``) forced on and off; ``NCCL_PROTO=Simple``; ``NCCL_BUFFSIZE``
+of 16 / 32 MiB, and 16 MiB with Simple.
+
+The verdict is persisted (:func:`persist`) keyed by a topology signature -- host, world
+size, GPUs visible, RCCL version -- in ``PDCC_RCCL_ENV_FILE`` (default: next to
+``PDCC_AUTOTUNE_FILE`` if that is set, else ``~/.cache/pdcc/rccl_env.json``), and every
+process of this library applies it (:func:`apply_persisted`, from the backend's creator)
+before its first RCCL communicator -- not only ``bench.py``. Settings the user made
+(``NCCL_*`` / ``PDCC_RCCL_*``) always win.
 """
 from __future__ import annotations
 
@@ -42,9 +51,23 @@ import tempfile
 import time
 
 MiB = 1 << 20
-BUFFSIZES = ("default", 8 * MiB, 16 * MiB, 32 * MiB)
-PROTOS = ("default", "Simple")
-_ENV_KEYS = ("NCCL_BUFFSIZE", "NCCL_PROTO")
+# NCCL / RCCL variable -> the PDCC_RCCL_* name the backend forwards (csrc/device/rccl_comm.cpp)
+_PDCC_NAME = {"NCCL_BUFFSIZE": "PDCC_RCCL_BUFFSIZE", "NCCL_PROTO": "PDCC_RCCL_PROTO",
+              "NCCL_ALGO": "PDCC_RCCL_ALGO", "RCCL_MSCCL_ENABLE": "PDCC_RCCL_MSCCL"}
+_ENV_KEYS = tuple(_PDCC_NAME)
+# (name, setting): one dimension at a time from RCCL's defaults (ALGO and MSCCL are the all-pairs /
+# tree alternatives SURVEY.md §5.8 asks for), then the buffer sizes that won before
+_GRID = (
+    ("default", {}),
+    ("algo=Ring", {"NCCL_ALGO": "Ring"}),
+    ("algo=Tree", {"NCCL_ALGO": "Tree"}),
+    ("msccl=1", {"RCCL_MSCCL_ENABLE": "1"}),
+    ("msccl=0", {"RCCL_MSCCL_ENABLE": "0"}),
+    ("proto=Simple", {"NCCL_PROTO": "Simple"}),
+    ("buffsize=16MiB", {"NCCL_BUFFSIZE": str(16 * MiB)}),
+    ("buffsize=32MiB", {"NCCL_BUFFSIZE": str(32 * MiB)}),
+    ("buffsize=16MiB,proto=Simple", {"NCCL_BUFFSIZE": str(16 * MiB), "NCCL_PROTO": "Simple"}),
+)
 # torchrun's agent-store variables must not leak into the children: they rendezvous among
 # themselves on their own port, not through the parent job's agent
 _STRIP = ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
@@ -53,14 +76,91 @@ _STRIP = ("TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_R
 
 
 def points():
-    """The sweep grid, in run order: (name, {NCCL var: value or None = unset})."""
-    out = []
-    for proto in PROTOS:
-        for bs in BUFFSIZES:
-            env = {"NCCL_BUFFSIZE": None if bs == "default" else str(bs),
-                   "NCCL_PROTO": None if proto == "default" else proto}
-            name = f"buffsize={'default' if bs == 'default' else f'{bs // MiB}MiB'},proto={proto}"
-            out.append((name, env))
+    """The sweep grid, in run order: (name, {variable: value or None = unset})."""
+    return [(name, {k: over.get(k) for k in _ENV_KEYS}) for name, over in _GRID]
+
+
+def user_set() -> list:
+    """RCCL settings the user made (their own NCCL_* or this library's PDCC_RCCL_* names)."""
+    return [k for k in _ENV_KEYS + tuple(_PDCC_NAME.values()) if os.environ.get(k)]
+
+
+def env_file() -> str | None:
+    """Where sweep verdicts persist (None: PDCC_RCCL_ENV_FILE=0 / off)."""
+    f = os.environ.get("PDCC_RCCL_ENV_FILE")
+    if f is not None:
+        return None if f.strip().lower() in ("", "0", "off", "none") else f
+    tune = os.environ.get("PDCC_AUTOTUNE_FILE")
+    if tune:
+        return tune + ".rccl_env.json"
+    return os.path.join(os.path.expanduser("~"), ".cache", "pdcc", "rccl_env.json")
+
+
+def signature(world: int, ngpu: int | None = None) -> str:
+    """Topology key of a verdict: host, world size, GPUs visible, RCCL version (no GPU init)."""
+    try:
+        import torch
+
+        if ngpu is None:
+            ngpu = torch.cuda.device_count()
+        ver = torch.cuda.nccl.version()
+        ver = ".".join(str(v) for v in ver) if isinstance(ver, tuple) else str(ver)
+    except Exception:
+        ver = "?"
+    return f"{socket.gethostname()}|w{world}|g{ngpu or 0}|rccl{ver}"
+
+
+def _load(path):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d if isinstance(d, dict) else {}
+    except (OSError, ValueError):
+        return {}
+
+
+def persist(sig: str, rec: dict, path: str | None = None) -> str | None:
+    """Record a sweep's verdict for `sig` (atomic replace; the applied env may be empty: RCCL's
+    defaults won). Returns the file written, or None."""
+    path = path or env_file()
+    if not path:
+        return None
+    d = _load(path)
+    d[sig] = {"env": rec.get("applied_env") or {}, "winner": rec.get("winner"), "bytes": rec.get("bytes"),
+              "p50_ms": {k: v.get("p50_ms") for k, v in rec.get("points", {}).items() if isinstance(v, dict)},
+              "time": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+    os.replace(tmp, path)
+    return path
+
+
+applied: dict = {}  # what apply_persisted set in this process (introspection)
+_checked = False
+
+
+def apply_persisted(world: int, ngpu: int | None = None, path: str | None = None) -> dict:
+    """Apply the persisted verdict for this topology to this process's environment, as the
+    PDCC_RCCL_* names the backend forwards at its first RCCL communicator. No-op if the user set
+    any RCCL variable, if no verdict matches, or once a verdict was applied. Returns what was set."""
+    global applied, _checked
+    if _checked or world < 2 and not os.environ.get("PDCC_RCCL_ENV_ANY_WORLD"):
+        return applied
+    _checked = True  # (RCCL reads its environment once per process: the first group decides)
+    path = path or env_file()
+    if not path or user_set():
+        return {}
+    ent = _load(path).get(signature(world, ngpu))
+    if not ent or not isinstance(ent.get("env"), dict):
+        return {}
+    out = {}
+    for k, v in ent["env"].items():
+        if k in _PDCC_NAME and v:
+            os.environ[_PDCC_NAME[k]] = str(v)
+            out[_PDCC_NAME[k]] = str(v)
+    applied = out
     return out
 
 
@@ -75,7 +175,8 @@ def _child_env(rank: int, world: int, local_rank: int, port: int, over: dict, nb
     env = {k: v for k, v in os.environ.items() if k not in _STRIP}
     for k in _ENV_KEYS:  # the point's setting, not whatever the parent job carries
         env.pop(k, None)
-        env.pop("PDCC_RCCL_" + k[5:], None)
+        env.pop(_PDCC_NAME[k], None)
+    env["PDCC_RCCL_ENV_FILE"] = "0"  # (a child never applies an earlier verdict)
     for k, v in over.items():
         if v is not None:
             env[k] = v
@@ -181,6 +282,11 @@ def sweep(store, rank: int, world: int, local_rank: int, nbytes: int = 1 << 30, 
         best, env = _decide(results)
         out_rec = {"points": results, "winner": best, "applied_env": env, "min_gain": 0.05,
                    "bytes": nbytes, "iters": iters, "elapsed_s": round(time.time() - t_start, 1)}
+        if best is not None:  # (only a sweep that measured something is a verdict)
+            try:
+                out_rec["persisted"] = {"file": persist(signature(world), out_rec), "signature": signature(world)}
+            except OSError as e:
+                out_rec["persisted"] = {"error": str(e)[:200]}
         store.set(f"{key}/record", json.dumps(out_rec))
         shutil.rmtree(tmp, ignore_errors=True)
     store.wait([f"{key}/record"], wait)
@@ -209,8 +315,11 @@ def sweep_local(world: int, nbytes: int = 1 << 30, budget_s: float = 300.0, poin
         results[name] = rec
     best, env = _decide(results)
     shutil.rmtree(tmp, ignore_errors=True)
-    return {"points": results, "winner": best, "applied_env": env, "bytes": nbytes, "iters": iters,
-            "elapsed_s": round(time.time() - t_start, 1)}
+    rec = {"points": results, "winner": best, "applied_env": env, "bytes": nbytes, "iters": iters,
+           "elapsed_s": round(time.time() - t_start, 1)}
+    if best is not None:
+        rec["persisted"] = {"file": persist(signature(world), rec), "signature": signature(world)}
+    return rec
 
 
 def _child():

@@ -111,8 +111,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--coll", default="all_reduce", help="all_reduce | all_gather | reduce_scatter")
     ap.add_argument("--algos", default="ipc,ipc_dyn",
-                    help="PDCC_ALGO values; ipc_dyn@N also sets PDCC_IPC_DYN=N (chunks per workgroup); a ~F "
-                         "suffix sets PDCC_TEST_IPC_FLAGS=F (ipc_dyn~8: round-4 claim loop, ~24: + uncached counters); "
+                    help="PDCC_ALGO values; ipc_dyn@N also sets PDCC_IPC_DYN=N (chunks per workgroup); "
                          "';KEY=VAL' suffixes set more environment (ipc_dyn;PDCC_IPC_DYN_MIN_ROWS=32)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
@@ -121,8 +120,8 @@ def main():
     res = {}
     for algo in a.algos.split(","):
         spec, *extra = algo.split(";")  # ;KEY=VAL: more environment for this engine's run
-        name, _, flags = spec.partition("~")  # ~N: PDCC_TEST_IPC_FLAGS=N (A/B hooks, kern::IpcCall::test_flags)
-        env = {"PDCC_ALGO": name.split("@")[0], "PDCC_AUTOTUNE": "0", "PDCC_TEST_IPC_FLAGS": flags or "0"}
+        name = spec
+        env = {"PDCC_ALGO": name.split("@")[0], "PDCC_AUTOTUNE": "0"}
         env.update(kv.split("=", 1) for kv in extra)
         if "@" in name:
             env["PDCC_IPC_DYN"] = name.split("@")[1]

@@ -139,14 +139,13 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--modes", default="zc,staged")
     ap.add_argument("--algo", default="ipc", help="PDCC_ALGO of the traced calls (ipc, ipc_dyn, ...)")
-    ap.add_argument("--test-flags", default="", help="PDCC_TEST_IPC_FLAGS (measurement hooks)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
 
     S = a.mib << 20
     W = a.world
     for mode in a.modes.split(","):
-        env = {"PDCC_ALGO": a.algo, "PDCC_TEST_IPC_FLAGS": a.test_flags or "0", "PDCC_IPC_TRACE": "64", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
+        env = {"PDCC_ALGO": a.algo, "PDCC_IPC_TRACE": "64", "PDCC_IPC_ZC": "0" if mode == "staged" else "1",
                "PDCC_AUTOTUNE": "0"}
         res = launch(work, W, args=(a.mib, a.iters), bind_device=True, timeout_s=120, env=env, join_timeout_s=400)
         # HBM bytes per call, all ranks together (one GPU): reads / writes

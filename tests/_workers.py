@@ -1409,11 +1409,15 @@ def zc_churn_probe(rank, size, device="cuda", allocs=40, n=(10 << 20) // 4 + 64)
         for i, t in enumerate(bufs):
             ok = ok and bool(torch.all(t == sum(r + i for r in range(size))))
     before = b.describe()
+    churn = b.zc_counters()  # (resolved: every churn call's outcome is in)
     dist.barrier()  # releases what the launcher's thread queued (evicted mappings)
     x = torch.ones(n, device=d)
     dist.all_reduce(x)
     torch.cuda.current_stream().synchronize()
-    return {"ok": ok, "algo": b.last_algo(), "desc": b.describe(), "before_barrier": before}
+    algo = b.last_algo()
+    last = b.zc_counters()
+    return {"ok": ok and bool(torch.all(x == size)), "algo": algo, "desc": b.describe(), "before_barrier": before,
+            "calls": 2 * allocs, "churn": churn, "last": last}
 
 
 def zc_burst_probe(rank, size, device="cuda", calls=64, n=(4 << 20) // 4):

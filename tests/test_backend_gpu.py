@@ -423,7 +423,11 @@ def test_conformance_pass_on_shared_gpu(world):
                      "wide/all_reduce", "coalesced/ipc/all_reduce_x64", "coalesced/ipc/all_gather_x64",
                      "coalesced/ipc/reduce_scatter_x64", "async_capped/ipc/all_reduce",
                      "async_capped/ipc_dyn/all_reduce", "raced/all_reduce/float32/SUM/24MiB",
-                     "raced/all_reduce/int32/BXOR/24MiB"):
+                     "raced/all_reduce/int32/BXOR/24MiB",
+                     # round 6: the copy-engine engine and the ReduceOps at zero-copy / bulk sizes
+                     "sdma/broadcast", "sdma/all_gather", "sdma/all_gather_list", "sdma/gather", "sdma/scatter",
+                     "sdma/all_to_all", "ops/ipc/all_reduce/PRODUCT/64MiB", "ops/ipc_push/all_reduce/MIN/4MiB",
+                     "ops/ipc_dyn/all_reduce/AVG/64MiB", "ops/ipc_staged/all_reduce/MAX/4MiB"):
             assert want in r["checks"], (want, sorted(r["checks"]))
         assert not r["skipped"], r["skipped"]
 
@@ -457,10 +461,24 @@ def test_zero_copy_eviction_churn(cache, zx):
     # their last launch (deferred, no hipDeviceSynchronize), every result exact; with the
     # device-side record exchange (zx=1: mapping-table entries dropped and re-filled under the
     # running kernels) and with the host gate only (PDCC_IPC_ZX=0)
+    # Verdict r5 Next #1: the engine label is the OUTCOME. Every churn call attempted zero copy and is
+    # counted once, as zero-copy or staged (a fresh export refused while the closing list is full runs
+    # staged); the final call's label says which it was, on both ranks alike.
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": cache, "PDCC_IPC_ZX": zx}
-    for r in _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120):
-        assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+    res = _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120)
+    for r in res:
+        assert r["ok"], r
+        ch, last = r["churn"], r["last"]
+        assert ch["zc_calls"] + ch["zc_fallbacks"] == r["calls"] and ch["zc_pending"] == 0, r
+        # (a 4-entry cache with no safe point but the waits: the closing list fills and fresh exports
+        # are refused -- 44 of 80 calls ran staged on the first run that could see it; 16 entries: none)
+        assert ch["zc_calls"] >= (r["calls"] // 2 if cache == "16" else 1), r
+        final_staged = last["zc_fallbacks"] - ch["zc_fallbacks"]
+        assert last["zc_calls"] + last["zc_fallbacks"] == r["calls"] + 1, r
+        assert r["algo"] == ("ipc_2shot" if final_staged else "ipc_2shot_zc"), r
         assert f"zx_ok={zx}" in r["desc"], r["desc"]
+    assert res[0]["algo"] == res[1]["algo"], (res[0]["algo"], res[1]["algo"])  # the group's outcome
+    assert [r["churn"]["zc_calls"] for r in res] == [res[0]["churn"]["zc_calls"]] * 2, res
 
 
 def test_zero_copy_device_exchange_selftest_gate():
@@ -468,7 +486,9 @@ def test_zero_copy_device_exchange_selftest_gate():
     # for the whole group (zx_ok=0), and zero-copy calls keep working through the host gate
     env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZX_SELFTEST_FAIL": "1"}
     for r in _gpu_launch(W.zc_churn_probe, 2, env=env, timeout_s=120):
-        assert r["ok"] and r["algo"] == "ipc_2shot_zc", r
+        assert r["ok"] and r["churn"]["zc_calls"] >= r["calls"] // 2, r
+        final_staged = r["last"]["zc_fallbacks"] - r["churn"]["zc_fallbacks"]
+        assert r["algo"] == ("ipc_2shot" if final_staged else "ipc_2shot_zc"), r
         assert "zx_ok=0" in r["desc"] and "zc_ok=1" in r["desc"], r["desc"]
 
 
@@ -555,13 +575,14 @@ def test_rccl_communicator_creation_is_bounded():
     assert "PDCC_TEST_RCCL_INIT_SKIP" in r1["first"], r1
 
 
-def test_rccl_env_sweep_children_run_on_the_gpu(monkeypatch):
+def test_rccl_env_sweep_children_run_on_the_gpu(monkeypatch, tmp_path):
     # the RCCL buffer/protocol pre-sweep's child ranks (utils/rccl_env.py) on a real GPU: one
     # rank (the box has one GPU; RCCL forced on its 1-rank communicator), a 64 MiB all_reduce
     # per point inside a 40 s budget -- the default point must run, on RCCL, with its p50
     from pytorch_distributed_collective_communication_amd.utils import rccl_env
 
     monkeypatch.setenv("PDCC_WORLD1_LOCAL", "0")
+    monkeypatch.setenv("PDCC_RCCL_ENV_FILE", str(tmp_path / "rccl_env.json"))
     rec = rccl_env.sweep_local(1, nbytes=64 << 20, budget_s=40.0, point_timeout_s=30.0, iters=3)
     first = rec["points"][rccl_env.points()[0][0]]
     assert isinstance(first, dict) and first["ok"], rec
@@ -569,7 +590,7 @@ def test_rccl_env_sweep_children_run_on_the_gpu(monkeypatch):
     assert rec["elapsed_s"] < 90, rec
     ran = [v for v in rec["points"].values() if isinstance(v, dict)]
     assert all(v["ok"] for v in ran), rec
-    assert any(v.get("env", {}).get("NCCL_BUFFSIZE") for v in ran[1:]) or len(ran) == 1, rec
+    assert any(v.get("env") for v in ran[1:]) or len(ran) == 1, rec  # (a non-default point ran with its setting)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -610,7 +631,8 @@ def test_zero_copy_refuses_allocations_with_size_bit31():
         assert r["big_ok"] and r["small_ok"], r
         assert r["big_s"] < 10.0, r  # (stalled: the 30 s spin timeout)
         assert r["big_refusals"] >= 1 and r["small_refusals"] == r["big_refusals"], r
-        assert r["small_engine"].endswith("_zc"), r
+        # verdict r5 Next #1: the refused call is labelled by what ran (staged), the next one zero-copy
+        assert not r["big_engine"].endswith("_zc") and r["small_engine"].endswith("_zc"), r
 
 
 def test_zero_copy_device_exchange_epoch_wraps():

@@ -19,18 +19,27 @@ def _fake_spawn(p50_by_point, fail_rank=None):
     names = [n for n, _ in rccl_env.points()]
 
     def spawn(env):
-        bs, proto = env.get("NCCL_BUFFSIZE"), env.get("NCCL_PROTO")
-        name = next(n for n, e in rccl_env.points() if e["NCCL_BUFFSIZE"] == bs and e["NCCL_PROTO"] == proto)
+        mine = {k: env.get(k) for k in rccl_env._ENV_KEYS}
+        name = next(n for n, e in rccl_env.points() if e == mine)
         out = env.get("PDCC_RCCL_ENV_CHILD_RESULT")
         rc = 1 if fail_rank is not None and int(env["RANK"]) == fail_rank and name == names[1] else 0
         rec = {"p50_ms": p50_by_point[name], "busbw_GBps": 1.0, "engine": "rccl",
-               "env": {k: v for k, v in (("NCCL_BUFFSIZE", bs), ("NCCL_PROTO", proto)) if v}}
+               "env": {k: v for k, v in mine.items() if v}}
+        assert env["PDCC_RCCL_ENV_FILE"] == "0"  # a child never applies an earlier verdict
         code = f"import json,sys; out={out!r}\nif out: json.dump({rec!r}, open(out, 'w'))\nsys.exit({rc})"
         assert env["PDCC_ALGO"] == "rccl" and "TORCHELASTIC_USE_AGENT_STORE" not in env
         return subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                                 text=True, start_new_session=True)
 
     return spawn
+
+
+@pytest.fixture(autouse=True)
+def _verdict_file(tmp_path, monkeypatch):
+    monkeypatch.setenv("PDCC_RCCL_ENV_FILE", str(tmp_path / "rccl_env.json"))
+    for k in rccl_env._ENV_KEYS + tuple(rccl_env._PDCC_NAME.values()):
+        monkeypatch.delenv(k, raising=False)
+    return tmp_path / "rccl_env.json"
 
 
 def _run(world, monkeypatch, p50, budget_s=60.0, fail_rank=None):
@@ -83,7 +92,39 @@ def test_sweep_budget_skips_the_rest(monkeypatch):
 
 
 def test_points_grid_matches_the_documented_sweep():
-    pts = rccl_env.points()
-    assert len(pts) == 8 and pts[0][1] == {"NCCL_BUFFSIZE": None, "NCCL_PROTO": None}
-    sizes = {e["NCCL_BUFFSIZE"] for _, e in pts}
-    assert sizes == {None, str(8 << 20), str(16 << 20), str(32 << 20)}
+    pts = dict(rccl_env.points())
+    assert len(pts) == 9 and pts["default"] == {k: None for k in rccl_env._ENV_KEYS}
+    # verdict r5 Next #3: the algorithm-level alternatives next to the buffer / protocol points
+    assert pts["algo=Ring"]["NCCL_ALGO"] == "Ring" and pts["algo=Tree"]["NCCL_ALGO"] == "Tree"
+    assert pts["msccl=1"]["RCCL_MSCCL_ENABLE"] == "1" and pts["msccl=0"]["RCCL_MSCCL_ENABLE"] == "0"
+    assert {e["NCCL_BUFFSIZE"] for e in pts.values()} == {None, str(16 << 20), str(32 << 20)}
+
+
+def test_verdict_persists_and_a_second_process_applies_it(monkeypatch, _verdict_file):
+    # verdict r5 Next #3: the sweep's winner is written keyed by topology, and a process that is not
+    # bench.py -- here a fresh interpreter making an ordinary process group -- applies it before its
+    # first RCCL communicator (as the PDCC_RCCL_* names the backend forwards); user settings win
+    names = [n for n, _ in rccl_env.points()]
+    p50 = {n: 10.0 for n in names}
+    p50["algo=Tree"] = 7.0
+    rec, env = _run(2, monkeypatch, p50)[0]
+    assert env == {"NCCL_ALGO": "Tree"} and rec["persisted"]["file"] == str(_verdict_file)
+    saved = json.loads(_verdict_file.read_text())
+    sig = rccl_env.signature(2)
+    assert saved[sig]["env"] == {"NCCL_ALGO": "Tree"} and saved[sig]["winner"] == "algo=Tree"
+    # the same verdict for a 1-rank world (so one process can make the group), then a fresh process
+    rccl_env.persist(rccl_env.signature(1), rec)
+    code = ("import datetime, os, torch.distributed as dist\n"
+            "import pytorch_distributed_collective_communication_amd\n"
+            "dist.init_process_group('mi355x', rank=0, world_size=1, timeout=datetime.timedelta(seconds=30))\n"
+            "print('ALGO=' + os.environ.get('PDCC_RCCL_ALGO', '-'))\n"
+            "dist.destroy_process_group()\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {k: v for k, v in os.environ.items() if k not in rccl_env._STRIP}  # (no torchrun agent store)
+    base.update(PDCC_RCCL_ENV_ANY_WORLD="1", PYTHONPATH=root)
+    for extra, want in (({}, "ALGO=Tree"), ({"NCCL_PROTO": "Simple"}, "ALGO=-")):
+        port = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(rccl_env.free_port())}
+        r = subprocess.run([sys.executable, "-c", code], env={**base, **port, **extra},
+                           capture_output=True, text=True, timeout=120, cwd=root)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert want in r.stdout, (extra, r.stdout, r.stderr[-1000:])

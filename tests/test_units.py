@@ -115,7 +115,8 @@ def test_rccl_env_forwarding():
                                        "PDCC_IPC_ZC_CACHE": "3", "PDCC_ALGO": "ipc_push",
                                        "PDCC_RCCL_WIDE_CTAS": "56", "PDCC_RCCL_WIDE_MIN": "64M",
                                        "PDCC_IPC_GRID": "1024", "PDCC_IPC_WIDE_GRID": "0",
-                                       "PDCC_IPC_LL_MAX": "4K"}])
+                                       "PDCC_IPC_LL_MAX": "4K", "PDCC_IPC_SDMA": "0", "PDCC_SDMA_STREAMS": "5",
+                                       "PDCC_IPC_ZC_SIZE_GUARD": "0"}])
 def test_python_config_mirror_matches_the_backend(env):
     # the Python mirror (config.py) and the C++ Config read the same variables with the same defaults
     import re
@@ -127,7 +128,8 @@ def test_python_config_mirror_matches_the_backend(env):
     cpp = dict(re.findall(r"(\w+)=(\S+)", desc))
     for key in ("ipc_1shot_max", "ipc_2shot_max", "ipc_copy_max", "ipc_max_staging", "ipc_zc", "ipc_zc_min",
                 "ipc_zc_cache", "ipc_push", "ipc_spin_ms", "ipc_grid", "ipc_wide_grid", "ipc_ll_max", "autotune", "autotune_sample", "algo",
-                "rccl_wide_ctas", "rccl_wide_min", "a2a_list_agree", "ipc_zc_async"):
+                "rccl_wide_ctas", "rccl_wide_min", "a2a_list_agree", "ipc_zc_async", "ipc_sdma", "sdma_streams",
+                "ipc_zc_size_guard"):
         want = py[key]
         got = cpp[key].rstrip(",)")
         assert got == (str(int(want)) if isinstance(want, bool) else str(want)), (key, got, want)
@@ -173,3 +175,36 @@ def test_conformance_helpers():
     assert cf._close(torch.stack(xs).prod(0), xs, "PRODUCT", 4, "float32")
     b = [x.to(torch.bfloat16) for x in xs]
     assert cf._close(sum(x.float() for x in b).to(torch.bfloat16), b, "SUM", 4, "bfloat16")
+
+
+def test_conformance_zero_copy_check_fails_on_a_fallback():
+    # verdict r5 Next #1: a "*_zc" expectation fails when any call of the check ran staged, even if the
+    # label of its last call says zero-copy; the delta is in the record
+    from pytorch_distributed_collective_communication_amd.utils import conformance as cf
+
+    class FakeBackend:
+        def __init__(self, label, fallback_per_call):
+            self.label, self.step, self.n = label, fallback_per_call, 0
+
+        def last_algo(self):
+            return self.label
+
+        def zc_counters(self):
+            return {"zc_calls": 5, "zc_fallbacks": self.n}
+
+        def run(self):
+            self.n += self.step
+            return True
+
+    P = cf._Pass(0, 1, "cpu", deadline_s=60)
+    ok_b, bad_b, lab_b = FakeBackend("ipc_2shot_zc", 0), FakeBackend("ipc_2shot_zc", 1), FakeBackend("ipc_2shot", 0)
+    P.check("zc/ok", ok_b, ok_b.run, expect_engine="ipc_2shot_zc")
+    P.check("zc/fell_back", bad_b, bad_b.run, expect_engine="ipc_2shot_zc")
+    P.check("zc/staged_label", lab_b, lab_b.run, expect_engine="ipc_2shot_zc")
+    P.check("staged/any", bad_b, bad_b.run, expect_engine="ipc_2shot")  # (not a zero-copy expectation)
+    r = P.result()
+    assert r["checks"]["zc/ok"] == {"ok": True, "engine": "ipc_2shot_zc", "want": "ipc_2shot_zc", "zc_fallbacks": 0}
+    assert r["checks"]["zc/fell_back"]["ok"] is False and r["checks"]["zc/fell_back"]["zc_fallbacks"] == 1
+    assert r["checks"]["zc/staged_label"]["ok"] is False
+    assert r["checks"]["staged/any"]["ok"] is False  # (label "ipc_2shot_zc" is not "ipc_2shot")
+    assert sorted(r["failed"]) == ["staged/any", "zc/fell_back", "zc/staged_label"]
