@@ -32,6 +32,19 @@ def _load_native():
     """Import the in-tree native extension ``_C``; fail loudly if it is missing."""
     global _native_mod
     if _native_mod is None:
+        so = os.environ.get("PDCC_NATIVE_SO")  # another build of _C (the sanitized one, tests/test_sanitizers.py)
+        if so:
+            import importlib.util
+            import sys
+
+            spec = importlib.util.spec_from_file_location(__name__ + "._C", so)
+            if spec is None or not os.path.exists(so):
+                raise ImportError(f"PDCC_NATIVE_SO={so}: no such extension")
+            mod = importlib.util.module_from_spec(spec)
+            sys.modules[__name__ + "._C"] = mod
+            spec.loader.exec_module(mod)
+            _native_mod = mod
+            return _native_mod
         try:
             _native_mod = importlib.import_module(__name__ + "._C")
         except ImportError as e:  # pragma: no cover - exercised only on broken installs

@@ -28,8 +28,19 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PDCC_ARCH", "gfx950")
 
 
-def ext_path() -> str:
-    return os.path.join(PKG_DIR, "_C" + sysconfig.get_config_var("EXT_SUFFIX"))
+SAN_DIR = os.path.join(ROOT, "build", "san_ext")
+SAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize=vptr",
+             "-fno-sanitize-recover=undefined"]
+
+
+def ext_path(sanitize: bool = False) -> str:
+    name = "_C" + sysconfig.get_config_var("EXT_SUFFIX")
+    return os.path.join(SAN_DIR, name) if sanitize else os.path.join(PKG_DIR, name)
+
+
+def asan_runtime() -> str:
+    """The ASan runtime the sanitized extension links against (LD_PRELOAD it into Python)."""
+    return subprocess.run(["g++", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
 
 
 def _torch_dirs():
@@ -64,9 +75,10 @@ def _headers_mtime(sub: str) -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
-def _obj(src: str) -> str:
+def _obj(src: str, sanitize: bool = False) -> str:
     rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
-    return os.path.join(BUILD, rel + ".o")
+    # (the sanitized variant instruments the host C++ only: the gfx950 kernels are shared)
+    return os.path.join(BUILD + ("_san" if sanitize and not src.endswith(".hip") else ""), rel + ".o")
 
 
 def _run(cmd, verbose):
@@ -78,12 +90,15 @@ def _run(cmd, verbose):
     return r.stdout
 
 
-def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -> str:
-    """Compile (incrementally) and link the extension; returns the .so path."""
+def build(jobs: int | None = None, force: bool = False, verbose: bool = False, sanitize: bool = False) -> str:
+    """Compile (incrementally) and link the extension; returns the .so path. `sanitize`: the host C++
+    with ASan + UBSan into build/san_ext/ (load it with PDCC_NATIVE_SO and the ASan runtime preloaded)."""
     tdir, tinc, tlib = _torch_dirs()
     import torch
 
     os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(BUILD + "_san", exist_ok=True)
+    os.makedirs(SAN_DIR, exist_ok=True)
     hip_srcs, cpp_srcs = _sources()
     py_inc = sysconfig.get_paths()["include"]
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
@@ -114,16 +129,17 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
 
     tasks = []
     for s in hip_srcs:
-        o = _obj(s)
+        o = _obj(s, sanitize)
         if stale(s, o, kern_hdr):
             tasks.append(
                 [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-c", s, "-o", o]
             )
     for s in cpp_srcs:
-        o = _obj(s)
+        o = _obj(s, sanitize)
         if stale(s, o, all_hdr):
             tasks.append(
-                ["g++", "-O2", "-g0", "-fPIC", "-std=c++17", "-Wno-deprecated-declarations", "-Wno-attributes"]
+                ["g++"] + (SAN_FLAGS if sanitize else ["-O2", "-g0"])
+                + ["-fPIC", "-std=c++17", "-Wno-deprecated-declarations", "-Wno-attributes"]
                 + common_defs
                 + incs
                 + ["-c", s, "-o", o]
@@ -134,11 +150,11 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False) -
             for f in futs:
                 f.result()
 
-    objs = [_obj(s) for s in hip_srcs + cpp_srcs]
-    out = ext_path()
+    objs = [_obj(s, sanitize) for s in hip_srcs + cpp_srcs]
+    out = ext_path(sanitize)
     if force or tasks or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
         link = (
-            ["g++", "-shared", "-o", out + ".tmp"]
+            ["g++", "-shared"] + (["-fsanitize=address,undefined"] if sanitize else []) + ["-o", out + ".tmp"]
             + objs
             + [
                 f"-L{tlib}",
@@ -168,8 +184,9 @@ def main(argv=None):
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--sanitize", action="store_true", help="ASan + UBSan host build into build/san_ext/")
     a = ap.parse_args(argv)
-    p = build(a.jobs, a.force, a.verbose)
+    p = build(a.jobs, a.force, a.verbose, a.sanitize)
     print(p)
 
 
