@@ -34,13 +34,13 @@ def _load_native():
     if _native_mod is None:
         so = os.environ.get("PDCC_NATIVE_SO")  # another build of _C (the sanitized one, tests/test_sanitizers.py)
         if so:
-            import importlib.util
             import sys
+            from importlib import util as _util
 
-            spec = importlib.util.spec_from_file_location(__name__ + "._C", so)
+            spec = _util.spec_from_file_location(__name__ + "._C", so)
             if spec is None or not os.path.exists(so):
                 raise ImportError(f"PDCC_NATIVE_SO={so}: no such extension")
-            mod = importlib.util.module_from_spec(spec)
+            mod = _util.module_from_spec(spec)
             sys.modules[__name__ + "._C"] = mod
             spec.loader.exec_module(mod)
             _native_mod = mod

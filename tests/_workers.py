@@ -1925,3 +1925,36 @@ def zc_size_guard_probe(rank, size, device="cuda", mib=2050):
         m2 = re.search(r"zc_size_refusals=(\d+)", b.describe())
         out[f"{tag}_refusals"] = int(m2.group(1)) if m2 else -1
     return out
+
+
+def distinct_suite(rank, size, device, phases, store_dir):
+    """One launch for many distinct-GPU checks (verdict r5 Next #6: the GPU suite's multi-GPU layer
+    in one process set per world size instead of one per parametrization). `phases` =
+    [(key, worker name, args, env)]: for each, the phase's environment is applied (the backend reads
+    its PDCC_* configuration when a group is made), the default group is re-made on a FileStore of its
+    own, and the worker runs; {key: result, or {"__error__": message}} per rank."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    out = {}
+    for k, (key, fname, args, env) in enumerate(phases):
+        saved = {n: os.environ.get(n) for n in env}
+        os.environ.update({n: str(v) for n, v in env.items()})
+        try:
+            if dist.is_initialized():
+                dist.destroy_process_group()
+            store = dist.FileStore(os.path.join(store_dir, f"phase{k}"), size)
+            dist.init_process_group("mi355x", store=store, rank=rank, world_size=size,
+                                    timeout=datetime.timedelta(seconds=120))
+            out[key] = globals()[fname](rank, size, *args)
+        except Exception as e:  # noqa: BLE001 - recorded per phase; the test that owns it fails
+            out[key] = {"__error__": f"{type(e).__name__}: {e}"[:800]}
+        finally:
+            for n, v in saved.items():
+                if v is None:
+                    os.environ.pop(n, None)
+                else:
+                    os.environ[n] = v
+    return out

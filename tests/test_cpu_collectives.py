@@ -150,3 +150,23 @@ def test_coalesced_collectives_are_one_operation(world):
 def test_coalesced_direct_entry_points():
     for r in launch(W.coalesced_direct, 3, args=("cpu",)):
         assert r == {"ag": True, "rs": True}, r
+
+
+def test_distinct_suite_machinery(tmp_path):
+    # verdict r5 Next #6: the multi-GPU layer runs every check of a world size in one launch
+    # (tests/test_multi_gpu.py); the phase machinery itself -- env per phase, the default group
+    # re-made on a FileStore per phase, per-phase error capture -- on the host transport here
+    from tests.test_multi_gpu import _plan
+
+    phases = (("golden", "golden", ("cpu",), {"PDCC_LOG_LEVEL": "0"}),
+              ("large", "large", ("cpu",), {"PDCC_SHM_SLOT_BYTES": "1M"}),
+              ("bad", "no_such_worker", (), {}),
+              ("golden_again", "golden", ("cpu",), {}))
+    res = launch(W.distinct_suite, 2, args=("cpu", phases, str(tmp_path)))
+    for r, got in enumerate(res):
+        assert got["golden"] == W.expected_golden(r, 2) == got["golden_again"], got
+        assert all(got["large"].values()), got["large"]
+        assert "KeyError" in got["bad"]["__error__"], got["bad"]
+    for w in (2, 3, 4, 8):  # every world size of the GPU layer has a plan, keys unique
+        keys = [k for k, *_ in _plan(w, str(tmp_path))]
+        assert keys and len(keys) == len(set(keys)), (w, keys)
