@@ -817,6 +817,8 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
           enqueue_allreduce(Algo::HOST, h, kd, ko, nd, no, nok, op, root, rooted, ds, cs, to);
           enqueue_allreduce(cands[0], g, kd, ko, nd, no, nok, op, root, rooted, ds, cs, to);
           PDCC_HIP(hipStreamSynchronize(cs));
+          // (a partial sanity check: the prefix runs the protocol of its own size, not the key's -- the
+          // raced variants are then checked against the full-size reference run, results_match above)
           return results_match(h, g, op, size_);
         });
   });
@@ -873,7 +875,16 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
     const hipStream_t cs = current_stream(ds.device);
     return autotune(
         key, bytes, ds, cands, [&](size_t k) { enqueue_broadcast(cands[k], sc[k], root, ds, cs, to); },
-        [&](size_t r, size_t k) { return at::equal(sc[r], sc[k]); });
+        [&](size_t r, size_t k) { return at::equal(sc[r], sc[k]); },
+        [&] {  // IPC as the reference: itself vs the host transport on a <= kHostTuneMax prefix (a
+               // partial sanity check: the prefix takes the protocol of its own size)
+          const int64_t m = sample_numel(w.numel(), w.element_size(), kHostTuneMax);
+          at::Tensor h = w.reshape({-1}).narrow(0, 0, m).clone(), g = h.clone();
+          enqueue_broadcast(Algo::HOST, h, root, ds, cs, to);
+          enqueue_broadcast(cands[0], g, root, ds, cs, to);
+          PDCC_HIP(hipStreamSynchronize(cs));
+          return at::equal(h, g);
+        });
   });
   if (a == Algo::HOST) {
     enqueue_broadcast(Algo::HOST, w, root, ds, current_stream(ds.device), to);
@@ -929,7 +940,20 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
     const hipStream_t cs = current_stream(ds.device);
     return autotune(
         key, bytes, ds, cands, [&](size_t k) { enqueue_allgather(cands[k], si, sc[k], root, rooted, ds, cs, to); },
-        [&](size_t r, size_t k) { return lists_equal(sc[r], sc[k]); });
+        [&](size_t r, size_t k) { return lists_equal(sc[r], sc[k]); },
+        [&] {  // IPC as the reference: exact against the host transport on a <= kHostTuneMax prefix
+          const int64_t m = sample_numel(wi.numel(), wi.element_size(), kHostTuneMax, size_);
+          const at::Tensor pi = wi.reshape({-1}).narrow(0, 0, m);
+          std::vector<at::Tensor> h, g;
+          if (receiver) {
+            h = scratch_outputs(wi.options(), size_, m, flat);
+            g = scratch_outputs(wi.options(), size_, m, flat);
+          }
+          enqueue_allgather(Algo::HOST, pi, h, root, rooted, ds, cs, to);
+          enqueue_allgather(cands[0], pi, g, root, rooted, ds, cs, to);
+          PDCC_HIP(hipStreamSynchronize(cs));
+          return lists_equal(h, g);
+        });
   });
   if (a == Algo::HOST) {
     enqueue_allgather(Algo::HOST, wi, wo, root, rooted, ds, current_stream(ds.device), to);

@@ -23,7 +23,10 @@ import sysconfig
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(ROOT, "csrc")
-BUILD = os.path.join(ROOT, "build", "obj")
+# PDCC_OFFLOAD_COMPRESS=1 (default): the gfx950 code objects go into the fat binary compressed
+# (clang --offload-compress; the runtime inflates them when the library loads): the .so shrinks ~6x
+COMPRESS = os.environ.get("PDCC_OFFLOAD_COMPRESS", "1") not in ("0", "")
+BUILD = os.path.join(ROOT, "build", "objz" if COMPRESS else "obj")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PDCC_ARCH", "gfx950")
 
@@ -132,7 +135,8 @@ def build(jobs: int | None = None, force: bool = False, verbose: bool = False, s
         o = _obj(s, sanitize)
         if stale(s, o, kern_hdr):
             tasks.append(
-                [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{CSRC}", "-c", s, "-o", o]
+                [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", f"-I{CSRC}"]
+                + (["--offload-compress"] if COMPRESS else []) + ["-c", s, "-o", o]
             )
     for s in cpp_srcs:
         o = _obj(s, sanitize)

@@ -59,8 +59,31 @@ def _backend_options(backend):
     return _options_cls(BACKEND_NAME, datetime.timedelta(milliseconds=backend.timeout_ms()))
 
 
+_bound = False
+
+
+def bind_local_rank() -> int | None:
+    """``run.py --nproc`` ranks (PDCC_BIND_LOCAL_RANK=1): make GPU ``LOCAL_RANK % count`` this process's
+    device at its first process group, unless the script already picked one. Returns the device bound."""
+    global _bound
+    if _bound or os.environ.get("PDCC_BIND_LOCAL_RANK") != "1":
+        return None
+    _bound = True
+    import torch
+
+    n = torch.cuda.device_count()  # (does not initialise the GPU on this runtime)
+    if n == 0:
+        return None
+    if torch.cuda.is_initialized() and torch.cuda.current_device() != 0:
+        return None  # the script chose its device itself
+    d = int(os.environ.get("LOCAL_RANK", "0")) % n
+    torch.cuda.set_device(d)
+    return d
+
+
 def _create(dist_opts, backend_opts):
     C = _native()
+    bind_local_rank()
     # an earlier RCCL environment sweep's verdict for this topology (utils/rccl_env.py), before the
     # process's first RCCL communicator reads its environment
     from ..utils import rccl_env

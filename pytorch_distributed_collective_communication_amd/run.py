@@ -11,6 +11,9 @@ Two modes:
   ``RANK/WORLD_SIZE/LOCAL_RANK/MASTER_ADDR/MASTER_PORT`` exported, a free port
   picked (not main.py:93's fixed 29500), children's exit codes propagated and
   the survivors terminated as soon as one rank fails (main.py:107 ignores them).
+  Each rank is bound to GPU ``LOCAL_RANK % visible GPUs`` (local rank ->
+  hipSetDevice) when it makes its first process group, unless the script already
+  chose a device (``PDCC_BIND_LOCAL_RANK=1``, parallel/backend.py).
 """
 from __future__ import annotations
 
@@ -62,7 +65,7 @@ def main(argv=None) -> int:
     for r in range(a.nproc):
         e = dict(env)
         e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.nproc), MASTER_PORT=str(port),
-                 LOCAL_WORLD_SIZE=str(a.nproc))
+                 LOCAL_WORLD_SIZE=str(a.nproc), PDCC_BIND_LOCAL_RANK="1")
         procs.append(subprocess.Popen(cmd, env=e))
     rc = 0
     try:

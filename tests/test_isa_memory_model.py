@@ -38,11 +38,31 @@ def _so():
     return p
 
 
+def _compressed_code_objects(b, tmp):
+    """The gfx950 code objects of compressed bundles ("CCOB", clang --offload-compress, the default build):
+    each bundle's header holds its total size; clang-offload-bundler inflates and unbundles it."""
+    out, pos, k = [], 0, 0
+    while True:
+        i = b.find(b"CCOB", pos)
+        if i < 0:
+            return out
+        ver = struct.unpack_from("<H", b, i + 4)[0]
+        total = struct.unpack_from("<Q" if ver >= 3 else "<I", b, i + 8)[0]
+        src, dst = os.path.join(tmp, f"bundle{k}.ccob"), os.path.join(tmp, f"bundle{k}.co")
+        open(src, "wb").write(b[i:i + total])
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={src}", f"--output={dst}"], check=True)
+        out.append(open(dst, "rb").read())
+        pos, k = i + max(total, 4), k + 1
+
+
 def _code_objects(so, tmp):
     fat = os.path.join(tmp, "fatbin.bin")
     subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "-O", "binary", "--only-section=.hip_fatbin", so, fat],
                    check=True)
     b = open(fat, "rb").read()
+    if b.find(MAGIC) < 0 and b.find(b"CCOB") >= 0:
+        return _compressed_code_objects(b, tmp)
     out, pos = [], 0
     while True:
         i = b.find(MAGIC, pos)
