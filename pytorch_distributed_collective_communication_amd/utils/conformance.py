@@ -426,7 +426,10 @@ def run(rank: int, world: int, dev, deadline_s: float = 45.0, max_bytes: int = 6
         if world > 1 and ipc_ok:
             eng += ([("ipc", "ipc_2shot_zc"), ("ipc_dyn", "ipc_2shot_dyn_zc"), ("ipc_push", "ipc_push_zc"),
                      ("ipc_staged", "ipc_2shot")] if zc_ok else [("ipc", "ipc_2shot")])
-        _op_checks(P, g, gb, set_engine, rank, W, dev, eng, [b for b in (4 << 20, 64 << 20) if b <= max_bytes])
+        sizes = [b for b in (4 << 20, 64 << 20) if b <= max_bytes]
+        if not sizes:  # a small rehearsal (PDCC_BENCH_SMALL): RCCL's variants at the size it has
+            eng, sizes = [e for e in eng if e[0] == "rccl"], [max_bytes]
+        _op_checks(P, g, gb, set_engine, rank, W, dev, eng, sizes)
     if on_gpu and world > 1:
         _coalesced_checks(P, g, gb, set_engine, rank, W, dev, ("ipc",) * ipc_ok + ("rccl",) * rccl_ok)
         if ipc_ok:

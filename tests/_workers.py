@@ -1958,3 +1958,28 @@ def distinct_suite(rank, size, device, phases, store_dir):
                 else:
                     os.environ[n] = v
     return out
+
+
+def size_guard_vote_probe(rank, size, device="cuda"):
+    """rank 1 lifts the zero-copy size guard for a new group, rank 0 does not; the
+    group's first GPU collective votes, and both ranks end with the guard on (a guarded rank must never
+    import a record a rank without the guard exported)."""
+    import os
+    import re
+
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    if rank == 1:
+        os.environ["PDCC_IPC_ZC_SIZE_GUARD"] = "0"
+    g = dist.new_group(list(range(size)))
+    os.environ.pop("PDCC_IPC_ZC_SIZE_GUARD", None)
+    b = be.native_backend(g, "cuda")
+    before = re.search(r"ipc_zc_size_guard=(\d)", b.describe()).group(1)
+    x = torch.ones(1 << 20, device=_dev(device))
+    dist.all_reduce(x, group=g)
+    torch.cuda.synchronize()
+    after = re.search(r"ipc_zc_size_guard=(\d)", b.describe()).group(1)
+    return {"before": before, "after": after, "ok": bool(torch.all(x == size))}

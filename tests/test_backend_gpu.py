@@ -635,6 +635,13 @@ def test_zero_copy_refuses_allocations_with_size_bit31():
         assert not r["big_engine"].endswith("_zc") and r["small_engine"].endswith("_zc"), r
 
 
+def test_zero_copy_size_guard_is_voted_group_wide():
+    # the guard is lifted only if every rank lifts it
+    res = _gpu_launch(W.size_guard_vote_probe, 2, timeout_s=60)
+    assert [r["before"] for r in res] == ["1", "0"], res
+    assert all(r["after"] == "1" and r["ok"] for r in res), res
+
+
 def test_zero_copy_device_exchange_epoch_wraps():
     # the device-side exchange's per-rank epoch wraps from 2^32-1 to 1
     # (never 0, and the STORED word moves on too); before the fix two consecutive calls shared
