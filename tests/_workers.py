@@ -257,7 +257,8 @@ def stats_probe(rank, size):
     t = torch.ones(16)
     dist.all_reduce(t)
     st = backend.stats()
-    return {k: list(v) for k, v in st.items()}, backend.describe()
+    zc = dict(backend.native_backend(None, "cpu").zc_counters())  # (no GPU op: every counter 0)
+    return {k: list(v) for k, v in st.items()}, backend.describe(), zc, backend.last_algo()
 
 
 def timing_allreduce(rank, size, n=1 << 20, iters=20):

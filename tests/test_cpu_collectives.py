@@ -74,9 +74,10 @@ def test_debug_fingerprint_catches_shape_mismatch():
 
 def test_stats_and_describe():
     res = launch(W.stats_probe, 2)
-    st, desc = res[0]
+    st, desc, zc, last = res[0]
     assert st["allreduce/shm"][0] >= 1
     assert "ProcessGroupMI355X" in desc and "size=2" in desc
+    assert last == "shm" and zc["zc_calls"] == zc["zc_fallbacks"] == zc["zc_pending"] == 0, (last, zc)
 
 
 def test_peer_death_is_detected_quickly():
