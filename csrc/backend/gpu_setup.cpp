@@ -420,7 +420,9 @@ bool ProcessGroupMI355X::ipc_selftest(DeviceState& ds) {
   if (!all) {
     fprintf(stderr, "[pdcc r%d] IPC self-test failed (%s): group '%s' runs without the peer-memory path\n", rank_,
             ok ? "on another rank" : why.c_str(), group_name_.c_str());
-    ds.ipc.reset();  // every rank voted after its own kernels finished: nothing touches these buffers any more
+    // every rank voted after its own kernels finished: nothing touches these buffers any more
+    if (ds.ipc) ds.ipc->release(std::chrono::milliseconds(std::max<int64_t>(1, std::min<int64_t>(timeout_.count(), 30000))));
+    ds.ipc.reset();
     return false;
   }
   // zero-copy IPC (user buffers mapped per call and read in place): whole rows /

@@ -655,6 +655,7 @@ std::map<std::string, uint64_t> ProcessGroupMI355X::zc_counters() {
   out["zc_size_refusals"] = size_ref;
   out["zc_full_refusals"] = full_ref;
   out["zc_exchange_fallbacks"] = xchg_fallbacks;
+  out["ipc_stale_maps"] = IpcComm::stale_mappings();
   return out;
 }
 
@@ -725,6 +726,7 @@ std::string ProcessGroupMI355X::describe() {
       << ", zc_closing=" << (kv.second->ipc ? kv.second->ipc->zc_closing() : 0)
       << ", zc_full_refusals=" << (kv.second->ipc ? kv.second->ipc->zc_full_refusals() : 0)
       << ", zc_size_refusals=" << (kv.second->ipc ? kv.second->ipc->zc_size_refusals() : 0)
+      << ", ipc_stale_maps=" << IpcComm::stale_mappings()
       << ", async_capped=" << (kv.second->ipc ? kv.second->ipc->async_capped() : 0)
       << ", launcher_jobs=" << (kv.second->launcher ? kv.second->launcher->jobs : 0)
       << ", zc_fallbacks=" << (kv.second->launcher ? kv.second->launcher->fallbacks : 0);
@@ -781,6 +783,8 @@ void ProcessGroupMI355X::shutdown() {
     std::lock_guard<std::mutex> lk(init_mu_);
     for (auto& kv : devs_) {
       streams.push_back(kv.second->stream.stream());
+      // (synchronous collectives ran on the caller's stream)
+      streams.push_back(c10::hip::getCurrentHIPStreamMasqueradingAsCUDA((c10::DeviceIndex)kv.first).stream());
       for (auto& p : kv.second->pairs) streams.push_back(p.second->stream.stream());
     }
   }
@@ -796,6 +800,20 @@ void ProcessGroupMI355X::shutdown() {
     }
     (void)hipGetLastError();
   }
+  // Release the group's IPC memory now (collectively: every rank closes its mappings of the peers'
+  // buffers before any rank frees its own, IpcComm::release), not whenever the last reference goes
+  stop_launchers();
+  for (hipStream_t s : streams) (void)hipStreamSynchronize(s);
+  {
+    std::lock_guard<std::mutex> lk(init_mu_);
+    for (auto& kv : devs_) {
+      for (hipStream_t x : kv.second->sdma_side) (void)hipStreamSynchronize(x);
+      if (kv.second->ipc)
+        kv.second->ipc->release(std::min<std::chrono::milliseconds>(
+            std::chrono::duration_cast<std::chrono::milliseconds>(timeout_), std::chrono::milliseconds(30000)));
+    }
+  }
+  (void)hipGetLastError();
 }
 
 c10d::ErrorType ProcessGroupMI355X::getError() {

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 #include <torch/csrc/distributed/c10d/Store.hpp>
 
+#include <chrono>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -35,6 +36,20 @@ inline void store_barrier(const c10::intrusive_ptr<c10d::Store>& store, const st
   std::vector<std::string> keys;
   for (int r = 0; r < world; ++r) keys.push_back(key + "/" + std::to_string(r));
   store->wait(keys);
+}
+
+// The same with a deadline: false when some rank did not arrive in time (a peer that is gone).
+inline bool store_barrier_for(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank,
+                              int world, std::chrono::milliseconds deadline) {
+  try {
+    store->set(key + "/" + std::to_string(rank), std::vector<uint8_t>{1});
+    std::vector<std::string> keys;
+    for (int r = 0; r < world; ++r) keys.push_back(key + "/" + std::to_string(r));
+    store->wait(keys, deadline);
+    return true;
+  } catch (...) {
+    return false;
+  }
 }
 
 }  // namespace pdcc

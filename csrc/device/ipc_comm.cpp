@@ -2,10 +2,16 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <random>
+#include <thread>
 #include <utility>
 
 #include "comm_util.h"
@@ -19,29 +25,95 @@ namespace {
 // sub-allocate. Export (handle, offset of p from its allocation base) and add the
 // offset back after opening -- without it a second group's buffers would alias
 // the first group's on the peer side.
-std::vector<uint8_t> handle_bytes(void* p) {
+//
+// Every exported buffer also carries a random 64-bit nonce in its last 8 bytes, published with the
+// handle: the importer reads it back through the mapping it was given. Right after a group was
+// destroyed and the next one made, the runtime was seen handing a peer back the mapping of the
+// previous group's (freed) buffer for a fresh export -- the new group's flags and staging then lived
+// in stale memory on one side and its first 2-shot all-reduce returned wrong sums on a shared GPU
+// (tests/test_backend_gpu.py::test_distinct_suite_machinery_on_shared_gpu, profiles/r6/). A stale
+// mapping shows up as a wrong nonce: it is closed and opened again until the runtime has let go of it.
+constexpr size_t kNonceBytes = 64;  // reserved at the end of every exported buffer
+std::atomic<uint64_t> g_stale_maps{0};
+
+uint64_t fresh_nonce() {
+  static std::atomic<uint64_t> ctr{0};
+  static const uint64_t seed = [] {
+    std::random_device rd;
+    return ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 17);
+  }();
+  uint64_t z = seed + 0x9e3779b97f4a7c15ull * (++ctr);  // splitmix64
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return (z ^ (z >> 31)) | 1u;  // (never 0: zeroed memory never matches)
+}
+
+// PDCC_IPC_VA_LOG=1 (debug): every IPC buffer this process allocates, maps, frees or unmaps, with its
+// address range, on stderr
+bool va_log_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("PDCC_IPC_VA_LOG");
+    return e && *e == '1';
+  }();
+  return on;
+}
+void va_note(const char* what, void* p) {
+  if (!va_log_on() || !p) return;
+  hipDeviceptr_t base = nullptr;
+  size_t range = 0;
+  if (hipMemGetAddressRange(&base, &range, reinterpret_cast<hipDeviceptr_t>(p)) != hipSuccess) (void)hipGetLastError();
+  fprintf(stderr, "[pdcc va %d] %s %p base %p range %zu\n", (int)getpid(), what, p, (void*)base, range);
+}
+hipError_t ipc_close(void* m) {
+  va_note("close", m);
+  return hipIpcCloseMemHandle(m);
+}
+hipError_t dev_free(void* p) {
+  va_note("free", p);
+  return hipFree(p);
+}
+
+std::vector<uint8_t> handle_bytes(void* p, size_t bytes) {
   hipIpcMemHandle_t h;
   PDCC_HIP(hipIpcGetMemHandle(&h, p));
   hipDeviceptr_t base = nullptr;
   size_t range = 0;
   PDCC_HIP(hipMemGetAddressRange(&base, &range, reinterpret_cast<hipDeviceptr_t>(p)));
   const uint64_t off = static_cast<uint64_t>(static_cast<char*>(p) - static_cast<char*>(base));
-  std::vector<uint8_t> out(sizeof(h) + sizeof(off));
+  const uint64_t nonce = fresh_nonce(), at = bytes - sizeof(uint64_t);
+  PDCC_HIP(hipMemcpy(static_cast<char*>(p) + at, &nonce, sizeof(nonce), hipMemcpyHostToDevice));
+  std::vector<uint8_t> out(sizeof(h) + 3 * sizeof(uint64_t));
   std::memcpy(out.data(), &h, sizeof(h));
   std::memcpy(out.data() + sizeof(h), &off, sizeof(off));
+  std::memcpy(out.data() + sizeof(h) + 8, &nonce, sizeof(nonce));
+  std::memcpy(out.data() + sizeof(h) + 16, &at, sizeof(at));
   return out;
 }
 
 // returns {mapping to close later, usable pointer}
 std::pair<void*, void*> open_handle(const std::vector<uint8_t>& b) {
   hipIpcMemHandle_t h;
-  uint64_t off = 0;
-  if (b.size() != sizeof(h) + sizeof(off)) throw std::runtime_error("pdcc: malformed hipIpc handle in store");
+  uint64_t off = 0, nonce = 0, at = 0;
+  if (b.size() != sizeof(h) + 3 * sizeof(uint64_t)) throw std::runtime_error("pdcc: malformed hipIpc handle in store");
   std::memcpy(&h, b.data(), sizeof(h));
   std::memcpy(&off, b.data() + sizeof(h), sizeof(off));
-  void* p = nullptr;
-  PDCC_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-  return {p, static_cast<char*>(p) + off};
+  std::memcpy(&nonce, b.data() + sizeof(h) + 8, sizeof(nonce));
+  std::memcpy(&at, b.data() + sizeof(h) + 16, sizeof(at));
+  for (int attempt = 0;; ++attempt) {
+    void* p = nullptr;
+    PDCC_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    uint64_t seen = 0;
+    PDCC_HIP(hipMemcpy(&seen, static_cast<char*>(p) + off + at, sizeof(seen), hipMemcpyDeviceToHost));
+    if (seen == nonce) {
+      va_note("open", p);
+      return {p, static_cast<char*>(p) + off};
+    }
+    ++g_stale_maps;
+    (void)ipc_close(p);
+    if (attempt >= 50)
+      throw std::runtime_error("pdcc: hipIpcOpenMemHandle keeps returning a stale mapping of a peer's IPC buffer");
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
 }
 
 // Allocate `bytes` of device memory and export it. With two ranks on one device
@@ -54,7 +126,7 @@ void* alloc_exportable(size_t bytes, bool uncached, std::vector<uint8_t>& blob, 
   auto release = [&] {  // (deferred: hipFree synchronises the device, see IpcComm::defer_frees)
     for (void* q : refused) {
       if (defer) defer->push_back(q);
-      else hipFree(q);
+      else dev_free(q);
     }
   };
   for (int attempt = 0; attempt < 6; ++attempt) {
@@ -65,7 +137,8 @@ void* alloc_exportable(size_t bytes, bool uncached, std::vector<uint8_t>& blob, 
       PDCC_HIP(e);
     }
     try {
-      blob = handle_bytes(p);
+      blob = handle_bytes(p, bytes);
+      va_note(uncached ? "alloc-uncached" : "alloc", p);
       release();
       return p;
     } catch (const std::exception&) {
@@ -103,6 +176,8 @@ void check_blobs(const std::vector<std::vector<uint8_t>>& all, int self, const c
 
 }  // namespace
 
+uint64_t IpcComm::stale_mappings() { return g_stale_maps.load(); }
+
 IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world,
                  int device, size_t max_staging, uint64_t timeout_ms, bool shared_device, size_t zc_cache)
     : store_(store),
@@ -125,9 +200,9 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   std::vector<uint8_t> mine;
   std::string err;
   try {
-    const size_t sig = granule(kern::ipc_signal_bytes());
+    const size_t sig = granule(kern::ipc_signal_bytes() + kNonceBytes);
     my_flags_ = static_cast<uint32_t*>(alloc_exportable(sig, true, mine));
-    PDCC_HIP(hipMemset(my_flags_, 0, sig));
+    PDCC_HIP(hipMemset(my_flags_, 0, sig - kNonceBytes));  // (not the nonce at the end)
     // the dynamic protocols' own control words: ordinary device memory (only this device's blocks)
     PDCC_HIP(hipMalloc(reinterpret_cast<void**>(&dyn_ctl_), kern::kDynCtlBytes));
     PDCC_HIP(hipMemset(dyn_ctl_, 0, kern::kDynCtlBytes));
@@ -180,57 +255,80 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
 }
 
 IpcComm::~IpcComm() {
+  release(std::chrono::milliseconds(0));
+  if (err_host_) hipHostFree(err_host_);
+}
+
+// Teardown order across the group: every rank closes its mappings of the peers' buffers, the ranks
+// meet, and only then does each free what it exported. Freeing an exported buffer while a peer still
+// had it mapped (ranks sharing one GPU, dmabuf IPC) left device memory that the next allocations on
+// both sides were handed at once: the next group's first bulk all-reduce on the shared GPU read zeros
+// in place of a fresh tensor's values (tests/_workers.py::regroup_probe, profiles/r6/regroup/).
+// Without the meeting (no deadline given, or a peer that never arrives) the exported buffers are kept
+// (a leak of the signal area and staging, never a free under a peer's mapping).
+void IpcComm::release(std::chrono::milliseconds deadline) {
+  if (released_) return;
+  released_ = true;
   try {
     DeviceScope ds(device_);
     graph_mode_ = false;  // the group is gone: staging retired for captured graphs goes too
-    unmap_staging();
+    // 1. this rank's mappings of the peers' memory
+    for (void* m : staging_maps_)
+      if (m) ipc_close(m);
+    staging_maps_.clear();
+    peer_staging_.clear();
     for (auto& r : retired_) {
       for (void* m : r.maps)
-        if (m) hipIpcCloseMemHandle(m);
-      if (r.mine) hipFree(r.mine);
+        if (m) ipc_close(m);
+      r.maps.clear();
+      if (r.mine) parked_.push_back(r.mine);
     }
     retired_.clear();
-    for (void* q : deferred_free_) hipFree(q);
-    deferred_free_.clear();
     reap_closing(true);
-    std::lock_guard<std::mutex> il(imports_mu_);
-    for (auto& peer : zc_imports_)
-      for (auto& im : peer) {
-        if (im.last && im.last->ev) (void)hipEventSynchronize(im.last->ev);
-        if (im.map) hipIpcCloseMemHandle(im.map);
-      }
-    zc_imports_.clear();
+    {
+      std::lock_guard<std::mutex> il(imports_mu_);
+      for (auto& peer : zc_imports_)
+        for (auto& im : peer) {
+          if (im.last && im.last->ev) (void)hipEventSynchronize(im.last->ev);
+          if (im.map) ipc_close(im.map);
+        }
+      zc_imports_.clear();
+    }
     for (void* m : flags_maps_)
-      if (m) hipIpcCloseMemHandle(m);
-    if (my_flags_) hipFree(my_flags_);
-    if (dyn_ctl_) hipFree(dyn_ctl_);
-    if (err_host_) hipHostFree(err_host_);
+      if (m) ipc_close(m);
+    flags_maps_.clear();
+    peer_flags_.clear();
+    // 2. never exported: free now
+    for (void* q : deferred_free_) dev_free(q);
+    deferred_free_.clear();
+    if (dyn_ctl_) dev_free(dyn_ctl_);
+    dyn_ctl_ = nullptr;
     gate_last_.clear();
     if (gates_host_) hipHostFree(gates_host_);
+    gates_host_ = nullptr;
     if (ztab_host_) hipHostFree(ztab_host_);
+    ztab_host_ = nullptr;
     if (trace_host_) hipHostFree(trace_host_);
+    trace_host_ = nullptr;
+    // 3. exported: once every rank has closed its mappings of them
+    if (my_staging_) parked_.push_back(my_staging_);
+    my_staging_ = nullptr;
+    cap_ = 0;
+    if (my_flags_) parked_.push_back(reinterpret_cast<char*>(my_flags_));
+    my_flags_ = nullptr;
+    const bool met = deadline.count() > 0 && store_barrier_for(store_, key_ + "/ipc_release", rank_, world_, deadline);
+    if (met) {
+      for (char* q : parked_) dev_free(q);
+    } else if (!parked_.empty() && log_ >= 1) {
+      fprintf(stderr, "[pdcc r%d] ipc: the group ended without every rank's teardown: its %zu exported buffer(s) "
+              "stay allocated\n", rank_, parked_.size());
+    }
+    parked_.clear();
   } catch (...) {
   }
 }
 
 thread_local bool IpcComm::tls_defer_frees_ = false;
-
-void IpcComm::unmap_staging() {
-  if (graph_mode_ || tls_defer_frees_) {
-    // a captured graph has these buffers baked into its kernel arguments, or this is the
-    // IPC launcher's thread (hipFree / hipIpcCloseMemHandle synchronise the device, and
-    // streams wait on this thread): keep them alive until maintain() / the group's end
-    if (my_staging_) retired_.push_back({my_staging_, staging_maps_});
-  } else {
-    for (void* m : staging_maps_)
-      if (m) hipIpcCloseMemHandle(m);
-    if (my_staging_) hipFree(my_staging_);
-  }
-  staging_maps_.clear();
-  peer_staging_.clear();
-  my_staging_ = nullptr;
-  cap_ = 0;
-}
 
 void IpcComm::map_staging(size_t cap) {
   // the new buffer is allocated and exported while the old one and the peers'
@@ -239,34 +337,47 @@ void IpcComm::map_staging(size_t cap) {
   std::string err;
   char* fresh = nullptr;
   try {
-    fresh = static_cast<char*>(alloc_exportable(granule(cap), false, mine, tls_defer_frees_ ? &deferred_free_ : nullptr));
+    fresh = static_cast<char*>(
+        alloc_exportable(granule(cap + kNonceBytes), false, mine, tls_defer_frees_ ? &deferred_free_ : nullptr));
   } catch (const std::exception& e) {
     err = e.what();
     mine.clear();
   }
-  unmap_staging();
-  my_staging_ = fresh;
   const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_, mine);
   try {
     if (!err.empty()) throw std::runtime_error(err);
     check_blobs(all, rank_, "staging buffer");
   } catch (...) {
-    if (my_staging_) hipFree(my_staging_);  // nobody opened it: every rank stops before opening
-    my_staging_ = nullptr;
+    if (fresh) dev_free(fresh);  // nobody opened it: every rank stops before opening
     throw;
   }
-  cap_ = cap;
-  peer_staging_.assign(world_, nullptr);
-  staging_maps_.assign(world_, nullptr);
+  std::vector<char*> peers(world_, nullptr);
+  std::vector<void*> maps(world_, nullptr);
   for (int r = 0; r < world_; ++r) {
     if (r == rank_) {
-      peer_staging_[r] = my_staging_;
+      peers[r] = fresh;
       continue;
     }
     auto m = open_handle(all[r]);
-    staging_maps_[r] = m.first;
-    peer_staging_[r] = static_cast<char*>(m.second);
+    maps[r] = m.first;
+    peers[r] = static_cast<char*>(m.second);
   }
+  // the old staging: mappings closed here, then (once every rank has closed its own) freed -- see release()
+  char* old = my_staging_;
+  const bool retire = graph_mode_ || tls_defer_frees_;
+  if (retire) {
+    if (old) retired_.push_back({old, staging_maps_});
+  } else {
+    for (void* m : staging_maps_)
+      if (m) ipc_close(m);
+  }
+  my_staging_ = fresh;
+  staging_maps_ = std::move(maps);
+  peer_staging_ = std::move(peers);
+  cap_ = cap;
+  // (not freed here: a buffer a peer had mapped, freed while the group lives on, was followed by a later
+  // zero-copy import on the shared GPU reading the importer's own tensor -- parked until release())
+  if (!retire && old) parked_.push_back(old);
 }
 
 void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
@@ -490,7 +601,7 @@ void IpcComm::reap_closing(bool wait_all) {
   }
   for (auto& c : done) {
     if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
-    if (c.map) hipIpcCloseMemHandle(c.map);
+    if (c.map) ipc_close(c.map);
   }
   if (!done.empty()) {
     std::lock_guard<std::mutex> lk(closing_mu_);
@@ -554,11 +665,15 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
         ok = false;
         continue;
       }
+      va_note("open-zc", m);
       peer.push_back({all[r].id, m, nullptr, tab_insert(r, all[r].id, m)});
       it = peer.end() - 1;
     }
     zc_cur_ids_[r] = all[r].id;
     ptrs[r] = static_cast<char*>(it->map) + all[r].off;
+    if (va_log_on())
+      fprintf(stderr, "[pdcc va %d] zc r%d<-r%d id %llu map %p off %llu ptr %p mine %p\n", (int)getpid(), rank_, r,
+              (unsigned long long)all[r].id, it->map, (unsigned long long)all[r].off, (void*)ptrs[r], mine);
   }
   return ok;
 }
@@ -695,13 +810,13 @@ void IpcComm::maintain() {
   DeviceScope ds(device_);
   reap_closing(true);
   if (graph_mode_) return;
-  for (auto& r : retired_) {
+  for (auto& r : retired_) {  // (own buffers wait for the group's teardown: a peer may map them still)
     for (void* m : r.maps)
-      if (m) hipIpcCloseMemHandle(m);
-    if (r.mine) hipFree(r.mine);
+      if (m) ipc_close(m);
+    if (r.mine) parked_.push_back(r.mine);
   }
   retired_.clear();
-  for (void* q : deferred_free_) hipFree(q);
+  for (void* q : deferred_free_) dev_free(q);
   deferred_free_.clear();
 }
 

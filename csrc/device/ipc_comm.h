@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -37,6 +38,13 @@ class IpcComm {
   IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string& key, int rank, int world, int device,
           size_t max_staging, uint64_t timeout_ms, bool shared_device, size_t zc_cache = 16);
   ~IpcComm();
+  // Close every peer mapping and free every buffer now (idempotent; the destructor does it
+  // otherwise). Collective: this rank's mappings of the peers' memory are closed first, then the
+  // ranks meet through the store (within `deadline`), then each frees what it exported -- never
+  // while a peer may still map it. No deadline (the destructor) or a rank that does not arrive:
+  // the exported buffers stay allocated. The group's shutdown calls it once its streams are
+  // drained. Only the host error word stays (Works read it).
+  void release(std::chrono::milliseconds deadline);
   IpcComm(const IpcComm&) = delete;
   IpcComm& operator=(const IpcComm&) = delete;
 
@@ -182,12 +190,14 @@ class IpcComm {
   uint64_t zc_full_refusals() const { return full_refusals_.load(); }
   // exports refused because the allocation's size has bit 31 set (see zc_export)
   uint64_t zc_size_refusals() const { return size_refusals_.load(); }
+  // stale peer mappings the runtime handed back for fresh exports and that were re-opened
+  // (process-wide; see open_handle in ipc_comm.cpp)
+  static uint64_t stale_mappings();
   void set_zc_size_guard(bool on) { size_guard_ = on; }
   size_t zc_closing_limit() const { return closing_limit_; }
 
  private:
   void map_staging(size_t cap);
-  void unmap_staging();
   kern::IpcView view(const std::vector<char*>& bufs) const;
   // grow the staging for `call` if needed (refused while the stream is being captured)
   void prepare_staging(const kern::IpcCall& call, hipStream_t stream);
@@ -273,9 +283,11 @@ class IpcComm {
   std::atomic<uint64_t> full_refusals_{0};
   std::atomic<uint64_t> size_refusals_{0};
   bool size_guard_ = true;
+  bool released_ = false;
   mutable std::mutex imports_mu_;  // zc_imports_ (launcher thread imports, describe() counts)
   static thread_local bool tls_defer_frees_;
   std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread
+  std::vector<char*> parked_;         // exported buffers a peer may still map: freed by release()
   std::vector<uint64_t> zc_cur_ids_;  // per peer: the allocation id mapped by the last zc_import
   std::vector<ZcExport> zc_exports_;
   std::vector<std::vector<ZcImport>> zc_imports_;  // per peer

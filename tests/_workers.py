@@ -1984,3 +1984,146 @@ def size_guard_vote_probe(rank, size, device="cuda"):
     torch.cuda.synchronize()
     after = re.search(r"ipc_zc_size_guard=(\d)", b.describe()).group(1)
     return {"before": before, "after": after, "ok": bool(torch.all(x == size))}
+
+
+def bulk_diag(rank, size, device="cuda", n=3_000_017):
+    """Diagnostics of the bulk all_reduce: engine, mismatch count, first bad index / value."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    base = torch.arange(n, dtype=torch.float32, device=d) % 1000
+    t = base * (rank + 1)
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+    want = base * (size * (size + 1) // 2)
+    bad = (t != want).nonzero().flatten()
+    out = {"engine": be.native_backend(None, "cuda").last_algo(), "bad": int(bad.numel())}
+    if bad.numel():
+        i = int(bad[0])
+        out.update(first=i, last=int(bad[-1]), got=float(t[i]), want=float(want[i]),
+                   got_over_base=float(t[i] / base[i]) if float(base[i]) else None)
+    out["zc"] = dict(be.native_backend(None, "cuda").zc_counters())
+    return out
+
+
+def ll_small(rank, size, device="cuda", calls=20, kind="all_reduce"):
+    """`calls` small (LL-range) collectives of one kind, synchronised at the end."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ok = True
+    for i in range(calls):
+        t = torch.full((1024,), float(rank + 1 + i), device=d)
+        if kind == "all_reduce":
+            dist.all_reduce(t)
+            ok = ok and bool(torch.all(t == sum(r + 1 + i for r in range(size))))
+        elif kind == "broadcast":
+            dist.broadcast(t, src=0)
+            ok = ok and bool(torch.all(t == 1 + i))
+        elif kind == "reduce":
+            dist.reduce(t, dst=0)
+            ok = ok and (rank != 0 or bool(torch.all(t == sum(r + 1 + i for r in range(size)))))
+    torch.cuda.synchronize()
+    return ok
+
+
+def canary(rank, size, device="cuda", n=16 << 20, wait_s=1.0):
+    """Rogue-writer check: a fresh tensor filled with 7.0 must stay 7.0 while nothing runs."""
+    import time
+
+    import torch
+
+    d = _dev(device)
+    x = torch.full((n,), 7.0, device=d)
+    torch.cuda.synchronize()
+    time.sleep(wait_s)
+    torch.cuda.synchronize()
+    return int((x != 7.0).sum())
+
+
+def regroup_probe(rank, size, device="cuda", destroy_a=True, b_first=False, n=3_000_017, b_algo=None, sleep_s=0.0,
+                  repeat=1, warm=False):
+    """Group A runs small (LL) all_reduces, then group B (same members) a bulk all_reduce. Per call:
+    [mismatches of B's result, elements of `base` changed during the call, mismatches of the input
+    before the call, first and last bad index]. `destroy_a`: A is destroyed before B's call;
+    `b_first`: B is made before A runs anything; `warm`: B runs a 1-element all_reduce first."""
+    import torch
+    import torch.distributed as dist
+
+    d = _dev(device)
+    ranks = list(range(size))
+    b = dist.new_group(ranks) if b_first else None
+    a = dist.new_group(ranks)
+    for i in range(5):
+        t = torch.full((1024,), float(rank + 1), device=d)
+        dist.all_reduce(t, group=a)
+    torch.cuda.synchronize()
+    if destroy_a:
+        dist.destroy_process_group(a)
+    if b is None:
+        b = dist.new_group(ranks)
+    if b_algo:
+        from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+        be.native_backend(b, "cuda").set_algo(b_algo)
+    if sleep_s:
+        import time
+
+        time.sleep(sleep_s)
+    if warm:
+        w = torch.ones(1, device=d)
+        dist.all_reduce(w, group=b)
+    out = []
+    for _ in range(repeat):
+        base = torch.arange(n, dtype=torch.float32, device=d) % 1000
+        t = base * (rank + 1)
+        torch.cuda.synchronize()
+        base_h = base.cpu()
+        t_h = t.cpu()
+        pre = int((t_h != base_h * (rank + 1)).sum())
+        dist.all_reduce(t, group=b)
+        torch.cuda.synchronize()
+        bad = (t.cpu() != base_h * (size * (size + 1) // 2))
+        nz = bad.nonzero()
+        got = t.cpu()
+        exp = base_h * (size * (size + 1) // 2)
+        idx = nz.flatten()[:: max(1, len(nz) // 12)][:12].tolist()
+        from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+        out.append([int(bad.sum()), int((base.cpu() != base_h).sum()), pre,
+                    int(nz[0]) if len(nz) else -1, int(nz[-1]) if len(nz) else -1,
+                    [(i, float(got[i]), float(exp[i])) for i in idx], be.native_backend(b, "cuda").last_algo(),
+                    hex(t.data_ptr()), hex(base.data_ptr()), os.getpid()])
+    return out
+
+
+def zc_reuse_diag(rank, size, device="cuda"):
+    """The zero_copy worker's first steps with per-call diagnostics: the 4 all-reduces, then 10 fill +
+    all_reduce calls on one 2 MiB buffer: [mismatches, engine] per call."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    tile = 1024
+    tri = size * (size + 1) // 2
+    out = []
+    for n in (size * tile * 300, size * tile * 300 + 77, (1 << 20) // 4 + 3, 3 * size * tile * 256 + 1):
+        base = torch.arange(n, device=d, dtype=torch.float32) % 1000
+        t = base * (rank + 1)
+        dist.all_reduce(t)
+        out.append([int((t != base * tri).sum()), b.last_algo()])
+    x = torch.empty(size * tile * 256, device=d)
+    for _ in range(10):
+        x.fill_(rank + 1.0)
+        dist.all_reduce(x)
+        torch.cuda.synchronize()
+        bad = (x != tri).nonzero().flatten()
+        out.append([len(bad), b.last_algo(), bad[:4].tolist(), x[bad[:4]].tolist() if len(bad) else []])
+    return {"calls": out[3:6], "zc": be.zc_counters(None), "x": hex(x.data_ptr()), "pid": os.getpid()}

@@ -704,3 +704,29 @@ def test_shared_device_grid_widens_for_large_calls(mib, blocks):
     for r in _gpu_launch(W.phase_trace_probe, 2, args=("cuda", 3, mib), env=env, timeout_s=120):
         assert r["ok"] and r["engine"].startswith("ipc_2shot"), r
         assert r["blocks_exit"] == blocks and r["blocks_phase1"] == blocks, r
+
+
+def test_distinct_suite_machinery_on_shared_gpu(tmp_path):
+    # verdict r5 Next #6: the distinct-GPU layer (tests/test_multi_gpu.py) runs every check of a world
+    # size in one launch, re-making the default group per phase; rehearse that on one GPU with the
+    # phases that do not need distinct devices (IPC and LL engines, zero copy, conformance, ZeRO)
+    phases = (("golden/ipc", "golden", ("cuda",), {"PDCC_ALGO": "ipc"}),
+              ("zero_copy/ipc", "zero_copy", ("cuda",), {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": "4",
+                                                        "PDCC_IPC_1SHOT_MAX": "256K", "PDCC_IPC_MAX_STAGING": "8M"}),
+              ("ll", "ll_probe", ("cuda",), {"PDCC_ALGO": "ipc"}),
+              ("bulk/ipc", "large", ("cuda",), {"PDCC_ALGO": "ipc"}),
+              ("sync_after_async/auto", "async_then_sync", ("cuda",), {"PDCC_ALGO": "auto"}),
+              ("conformance", "conformance_probe", ("cuda",), {}),
+              ("zero_train", "zero_train", ("adam", 5, "cuda", "float32", False, 4096), {}))
+    res = _gpu_launch(W.distinct_suite, 2, args=("cuda", phases, str(tmp_path)), timeout_s=120)
+    for r, got in enumerate(res):
+        errs = {k: v["__error__"] for k, v in got.items() if isinstance(v, dict) and "__error__" in v}
+        assert not errs, errs
+        assert got["golden/ipc"] == W.expected_golden(r, 2)
+        for key in ("zero_copy/ipc", "ll", "bulk/ipc"):
+            assert all(got[key].values()), (r, key, {k: v for k, v in got[key].items() if v is not True})
+        assert all(got["sync_after_async/auto"]), got["sync_after_async/auto"]
+        assert got["conformance"]["all_ok"], {k: v for k, v in got["conformance"]["checks"].items() if not v["ok"]}
+    ref = W.zero_reference("adam")
+    for r in res:
+        torch.testing.assert_close(torch.tensor(r["zero_train"][0]), ref, rtol=1e-4, atol=1e-4)
