@@ -189,6 +189,7 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
       timeout_ticks_(timeout_ms * 100000ull),  // s_memrealtime runs at 100 MHz
       shared_device_(shared_device) {
   zc_imports_.assign(world, {});
+  keep_exports_ = shared_device;
   if (const char* lv = std::getenv("PDCC_LOG_LEVEL")) log_ = std::atoi(lv);
   shared_grid_ = std::max(1, 256 / std::max(1, world));
   shared_wide_grid_ = std::max(1, kSharedWideSlots / std::max(1, world) - 1);
@@ -254,6 +255,10 @@ IpcComm::IpcComm(const c10::intrusive_ptr<c10d::Store>& store, const std::string
   }
 }
 
+void IpcComm::drop_map(void* m) {
+  if (m) (void)ipc_close(m);
+}
+
 IpcComm::~IpcComm() {
   release(std::chrono::milliseconds(0));
   if (err_host_) hipHostFree(err_host_);
@@ -274,12 +279,12 @@ void IpcComm::release(std::chrono::milliseconds deadline) {
     graph_mode_ = false;  // the group is gone: staging retired for captured graphs goes too
     // 1. this rank's mappings of the peers' memory
     for (void* m : staging_maps_)
-      if (m) ipc_close(m);
+      if (m) drop_map(m);
     staging_maps_.clear();
     peer_staging_.clear();
     for (auto& r : retired_) {
       for (void* m : r.maps)
-        if (m) ipc_close(m);
+        if (m) drop_map(m);
       r.maps.clear();
       if (r.mine) parked_.push_back(r.mine);
     }
@@ -290,12 +295,12 @@ void IpcComm::release(std::chrono::milliseconds deadline) {
       for (auto& peer : zc_imports_)
         for (auto& im : peer) {
           if (im.last && im.last->ev) (void)hipEventSynchronize(im.last->ev);
-          if (im.map) ipc_close(im.map);
+          if (im.map) drop_map(im.map);
         }
       zc_imports_.clear();
     }
     for (void* m : flags_maps_)
-      if (m) ipc_close(m);
+      if (m) drop_map(m);
     flags_maps_.clear();
     peer_flags_.clear();
     // 2. never exported: free now
@@ -316,9 +321,11 @@ void IpcComm::release(std::chrono::milliseconds deadline) {
     cap_ = 0;
     if (my_flags_) parked_.push_back(reinterpret_cast<char*>(my_flags_));
     my_flags_ = nullptr;
-    const bool met = deadline.count() > 0 && store_barrier_for(store_, key_ + "/ipc_release", rank_, world_, deadline);
-    if (met) {
+    const bool met = !keep_exports_ && deadline.count() > 0 && store_barrier_for(store_, key_ + "/ipc_release", rank_, world_, deadline);
+    if (met && !keep_exports_) {
       for (char* q : parked_) dev_free(q);
+    } else if (keep_exports_) {
+      kept_exports_ += parked_.size();  // ranks sharing one GPU: see keep_exports_
     } else if (!parked_.empty() && log_ >= 1) {
       fprintf(stderr, "[pdcc r%d] ipc: the group ended without every rank's teardown: its %zu exported buffer(s) "
               "stay allocated\n", rank_, parked_.size());
@@ -343,6 +350,23 @@ void IpcComm::map_staging(size_t cap) {
     err = e.what();
     mine.clear();
   }
+  // the old staging goes before the exchange: this rank's mappings of the peers' old buffers closed, its
+  // own old buffer freed (kept instead while a captured graph or the launcher's thread may use it). This
+  // order is the one measured clean on a shared GPU: keeping the old buffers until the new ones were
+  // mapped everywhere, then closing / freeing (or parking) them, was followed by wrong results in later
+  // calls (profiles/r6/regroup/README.md)
+  if (graph_mode_ || tls_defer_frees_) {
+    if (my_staging_) retired_.push_back({my_staging_, staging_maps_});
+  } else {
+    for (void* m : staging_maps_)
+      if (m) drop_map(m);
+    if (my_staging_ && keep_exports_) ++kept_exports_;
+    else if (my_staging_) dev_free(my_staging_);
+  }
+  staging_maps_.clear();
+  peer_staging_.clear();
+  my_staging_ = nullptr;
+  cap_ = 0;
   const auto all = store_allgather(store_, key_ + "/ipc_stg/" + std::to_string(staging_gen_), rank_, world_, mine);
   try {
     if (!err.empty()) throw std::runtime_error(err);
@@ -351,33 +375,19 @@ void IpcComm::map_staging(size_t cap) {
     if (fresh) dev_free(fresh);  // nobody opened it: every rank stops before opening
     throw;
   }
-  std::vector<char*> peers(world_, nullptr);
-  std::vector<void*> maps(world_, nullptr);
+  my_staging_ = fresh;
+  cap_ = cap;
+  peer_staging_.assign(world_, nullptr);
+  staging_maps_.assign(world_, nullptr);
   for (int r = 0; r < world_; ++r) {
     if (r == rank_) {
-      peers[r] = fresh;
+      peer_staging_[r] = my_staging_;
       continue;
     }
     auto m = open_handle(all[r]);
-    maps[r] = m.first;
-    peers[r] = static_cast<char*>(m.second);
+    staging_maps_[r] = m.first;
+    peer_staging_[r] = static_cast<char*>(m.second);
   }
-  // the old staging: mappings closed here, then (once every rank has closed its own) freed -- see release()
-  char* old = my_staging_;
-  const bool retire = graph_mode_ || tls_defer_frees_;
-  if (retire) {
-    if (old) retired_.push_back({old, staging_maps_});
-  } else {
-    for (void* m : staging_maps_)
-      if (m) ipc_close(m);
-  }
-  my_staging_ = fresh;
-  staging_maps_ = std::move(maps);
-  peer_staging_ = std::move(peers);
-  cap_ = cap;
-  // (not freed here: a buffer a peer had mapped, freed while the group lives on, was followed by a later
-  // zero-copy import on the shared GPU reading the importer's own tensor -- parked until release())
-  if (!retire && old) parked_.push_back(old);
 }
 
 void IpcComm::ensure_staging(size_t bytes, hipStream_t stream) {
@@ -601,7 +611,7 @@ void IpcComm::reap_closing(bool wait_all) {
   }
   for (auto& c : done) {
     if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: close %p\n", rank_, c.map);
-    if (c.map) ipc_close(c.map);
+    if (c.map) drop_map(c.map);
   }
   if (!done.empty()) {
     std::lock_guard<std::mutex> lk(closing_mu_);
@@ -812,7 +822,7 @@ void IpcComm::maintain() {
   if (graph_mode_) return;
   for (auto& r : retired_) {  // (own buffers wait for the group's teardown: a peer may map them still)
     for (void* m : r.maps)
-      if (m) ipc_close(m);
+      if (m) drop_map(m);
     if (r.mine) parked_.push_back(r.mine);
   }
   retired_.clear();

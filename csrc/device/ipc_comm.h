@@ -193,6 +193,8 @@ class IpcComm {
   // stale peer mappings the runtime handed back for fresh exports and that were re-opened
   // (process-wide; see open_handle in ipc_comm.cpp)
   static uint64_t stale_mappings();
+  // exported buffers kept instead of freed (ranks sharing one GPU, see keep_exports_)
+  uint64_t kept_exports() const { return kept_exports_.load(); }
   void set_zc_size_guard(bool on) { size_guard_ = on; }
   size_t zc_closing_limit() const { return closing_limit_; }
 
@@ -284,6 +286,17 @@ class IpcComm {
   std::atomic<uint64_t> size_refusals_{0};
   bool size_guard_ = true;
   bool released_ = false;
+  // Ranks sharing one GPU: a buffer this rank exported is never freed (outgrown staging, the group's
+  // signal area and staging at release). A buffer a peer had mapped, unmapped there and then freed here
+  // -- in either order, also with a group-wide barrier between -- came back to both processes at once:
+  // the next group's fresh tensors were zeroed in place by a peer's memset and a later zero-copy import
+  // read the importer's own tensor. Never freeing avoided it, and so did never unmapping, but kept
+  // mappings of freed buffers later hung an LL poll (tests/_workers.py regroup_probe / bulk_pre_diag /
+  // zc_reuse_diag, profiles/r6/regroup/README.md). The memory stays with the process; distinct GPUs
+  // (another device's memory imported) free as usual.
+  bool keep_exports_ = false;
+  std::atomic<uint64_t> kept_exports_{0};
+  void drop_map(void* m);
   mutable std::mutex imports_mu_;  // zc_imports_ (launcher thread imports, describe() counts)
   static thread_local bool tls_defer_frees_;
   std::vector<void*> deferred_free_;  // refused exportable blocks allocated on the launcher's thread

@@ -42,18 +42,25 @@ def suite(name, phases):
     print(json.dumps({name: falses(r)}), flush=True)
 
 
+def raw(name, phases, env=None):
+    d = tempfile.mkdtemp()
+    try:
+        r = launch(W.distinct_suite, 2, args=("cuda", phases, d), bind_device=True, timeout_s=120, join_timeout_s=300,
+                   env=env or {})
+        r = [x.get("diag") for x in r]
+    except Exception as e:  # noqa: BLE001
+        r = str(e)[:600]
+    print(json.dumps({name: r}), flush=True)
+
+
 def main():
-    zc_env = {"PDCC_ALGO": "ipc", "PDCC_IPC_ZC_CACHE": "4", "PDCC_IPC_1SHOT_MAX": "256K", "PDCC_IPC_MAX_STAGING": "8M",
-              "PDCC_IPC_VA_LOG": "1"}
-    golden = ("golden/ipc", "golden", ("cuda",), {"PDCC_ALGO": "ipc"})
-    diag = ("diag", "zc_reuse_diag", ("cuda",), zc_env)
-    for i in range(8):
-        d = tempfile.mkdtemp()
-        r = launch(W.distinct_suite, 2, args=("cuda", (golden, diag), d), bind_device=True, timeout_s=120,
-                   join_timeout_s=300, env={"PDCC_IPC_VA_LOG": "1"})
-        print(json.dumps({f"#{i}": [x["diag"] for x in r]}), flush=True)
-        if any(c[0] for x in r for c in x["diag"]["calls"]):
-            break
+    ph = {"golden": ("golden/ipc", "golden", ("cuda",), {"PDCC_ALGO": "ipc"}),
+          "ll": ("ll", "ll_probe", ("cuda",), {"PDCC_ALGO": "ipc"}),
+          "diag": ("diag", "bulk_pre_diag", ("cuda",), {"PDCC_ALGO": "ipc"}),
+          "diag_host": ("diag", "bulk_pre_diag", ("cuda",), {"PDCC_ALGO": "host"})}
+    for names in (("ll", "diag"), ("golden", "diag"), ("golden", "ll", "diag")):
+        for i in range(2):
+            raw(" > ".join(names) + f" #{i}", tuple(ph[n] for n in names))
 
 
 if __name__ == "__main__":

@@ -2127,3 +2127,27 @@ def zc_reuse_diag(rank, size, device="cuda"):
         bad = (x != tri).nonzero().flatten()
         out.append([len(bad), b.last_algo(), bad[:4].tolist(), x[bad[:4]].tolist() if len(bad) else []])
     return {"calls": out[3:6], "zc": be.zc_counters(None), "x": hex(x.data_ptr()), "pid": os.getpid()}
+
+
+def bulk_pre_diag(rank, size, device="cuda", n=3_000_017):
+    """The default group's first bulk all_reduce: [result mismatches, input mismatches seen on the host
+    before the call, engine, first bad index, (got, want) there]."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    base = torch.arange(n, dtype=torch.float32, device=d) % 1000
+    t = base * (rank + 1)
+    torch.cuda.synchronize()
+    base_h = torch.arange(n, dtype=torch.float32) % 1000
+    pre = int((t.cpu() != base_h * (rank + 1)).sum())
+    dist.all_reduce(t)
+    torch.cuda.synchronize()
+    got = t.cpu()
+    want = base_h * (size * (size + 1) // 2)
+    bad = (got != want).nonzero().flatten()
+    i = int(bad[0]) if len(bad) else -1
+    return [len(bad), pre, be.native_backend(None, "cuda").last_algo(), i,
+            (float(got[i]), float(want[i])) if i >= 0 else None]
