@@ -2151,3 +2151,4 @@ def bulk_pre_diag(rank, size, device="cuda", n=3_000_017):
     i = int(bad[0]) if len(bad) else -1
     return [len(bad), pre, be.native_backend(None, "cuda").last_algo(), i,
             (float(got[i]), float(want[i])) if i >= 0 else None]
+

@@ -706,6 +706,21 @@ def test_shared_device_grid_widens_for_large_calls(mib, blocks):
         assert r["blocks_exit"] == blocks and r["blocks_phase1"] == blocks, r
 
 
+def test_group_remade_after_ipc_teardown_on_shared_gpu(tmp_path):
+    # a group that ran the IPC path (self-test, LL, subgroups) is destroyed and the default group re-made:
+    # the next group's fresh tensors must hold what was written (freeing exported buffers a peer had
+    # mapped handed their memory to both processes: profiles/r6/regroup/README.md), and its first bulk
+    # all-reduce must be exact; ranks sharing the GPU keep their exported buffers instead
+    phases = (("golden/ipc", "golden", ("cuda",), {"PDCC_ALGO": "ipc"}),
+              ("ll", "ll_probe", ("cuda",), {"PDCC_ALGO": "ipc"}),
+              ("diag", "bulk_pre_diag", ("cuda",), {"PDCC_ALGO": "ipc"}))
+    res = _gpu_launch(W.distinct_suite, 2, args=("cuda", phases, str(tmp_path)), timeout_s=120)
+    for got in res:
+        bad, pre, engine = got["diag"][:3]
+        assert (bad, pre) == (0, 0), got["diag"]
+        assert engine.startswith("ipc_2shot"), engine
+
+
 def test_distinct_suite_machinery_on_shared_gpu(tmp_path):
     # verdict r5 Next #6: the distinct-GPU layer (tests/test_multi_gpu.py) runs every check of a world
     # size in one launch, re-making the default group per phase; rehearse that on one GPU with the
