@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""Isolate a failing bulk all_reduce in a group made after another group of the same ranks ran small
-(LL) collectives (tests/_workers.py regroup_probe / distinct_suite), ranks sharing one GPU."""
+"""Re-made groups on a shared GPU: runs tests/_workers.py::distinct_suite with a sequence of phases (each
+re-makes the default group) and reports the last phase's diagnostics -- `bulk_pre_diag` (the fresh input
+checked on the host before the call, then the result), `zc_reuse_diag`, `regroup_probe`. The probes behind
+profiles/r6/regroup/README.md; edit main() for other phase sequences.
+
+    python scripts/suite_probe.py        (2 ranks on GPU 0)
+"""
 import json
 import os
 import sys
