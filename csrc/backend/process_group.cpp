@@ -393,6 +393,18 @@ ProcessGroupMI355X::ProcessGroupMI355X(const c10::intrusive_ptr<c10d::Store>& st
   const std::string h(host);
   const auto all = store_allgather(store_, "pdcc/topo", rank, size, std::vector<uint8_t>(h.begin(), h.end()));
   for (const auto& v : all) same_host_ = same_host_ && (std::string(v.begin(), v.end()) == h);
+  // The store's server usually lives in rank 0's process: rank 0 leaves construction only once every rank
+  // has read the records above, so a job without a single collective (the reference's hello_world,
+  // main.py:86-87) cannot end rank 0 -- and the server with it -- under a peer still reading them
+  // (seen as "Failed to recv ... Connection was likely closed" in a peer's constructor)
+  if (size > 1) {
+    store_->add("pdcc/topo_read", 1);
+    if (rank == 0) {
+      const auto deadline = std::chrono::steady_clock::now() + timeout_;
+      while (store_->add("pdcc/topo_read", 0) < size && std::chrono::steady_clock::now() < deadline)
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+  }
   if (cfg_.log_level >= 1 && rank == 0)
     fprintf(stderr, "[pdcc] group '%s' size=%d same_host=%d %s\n", group_name_.c_str(), size, (int)same_host_,
             cfg_.describe().c_str());
