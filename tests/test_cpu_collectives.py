@@ -168,6 +168,15 @@ def test_distinct_suite_machinery(tmp_path):
         assert got["golden"] == W.expected_golden(r, 2) == got["golden_again"], got
         assert all(got["large"].values()), got["large"]
         assert "KeyError" in got["bad"]["__error__"], got["bad"]
+    import inspect
+
     for w in (2, 3, 4, 8):  # every world size of the GPU layer has a plan, keys unique
-        keys = [k for k, *_ in _plan(w, str(tmp_path))]
+        plan = _plan(w, str(tmp_path))
+        keys = [k for k, *_ in plan]
         assert keys and len(keys) == len(set(keys)), (w, keys)
+        for key, fname, args, env in plan:  # every phase names a worker whose signature takes its arguments
+            fn = getattr(W, fname, None)
+            assert callable(fn), (w, key, fname)
+            inspect.signature(fn).bind(0, w, *args)
+            assert all(isinstance(k, str) and k.startswith(("PDCC_", "NCCL_", "RCCL_", "GPU_", "HSA_"))
+                       for k in env), (w, key, env)
