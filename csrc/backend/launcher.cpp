@@ -103,6 +103,14 @@ uint64_t ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& cal
                                        size_t unit, size_t body, size_t per_call_max, hipStream_t s) {
   IpcComm& ic = ipc(ds);
   hp_.lap(HostStage::ENQUEUE);
+  // Evicted mappings are only queued on the launcher's thread; close the finished ones here, on the
+  // submitting thread, before this call's export: with every call gated (no inline exchange, no
+  // barrier) the closing lists otherwise only grow, and at W = 8 (seven peers' entries per eviction)
+  // a run of fresh buffers filled them within ~30 calls and every later fresh export was refused
+  // (staged; conformance's op checks, profiles/r6/plan_rehearsal_w8.jsonl). Every earlier call's
+  // exchange job is queued already, so the device synchronisation a close implies cannot wait on
+  // this thread.
+  if (ic.zc_closing() > 0) ic.reap_closing(false);
   const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, false);
   hp_.lap(HostStage::ZC_EXPORT);
   const uint64_t t = ic.gate_reserve();

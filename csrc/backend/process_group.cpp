@@ -652,11 +652,13 @@ std::map<std::string, uint64_t> ProcessGroupMI355X::zc_counters() {
     out["zc_fallbacks"] = zc_staged_calls_;
     out["zc_pending"] = pending_.size();
   }
-  uint64_t size_ref = 0, full_ref = 0, xchg_fallbacks = 0, kept = 0;
+  uint64_t size_ref = 0, full_ref = 0, xchg_fallbacks = 0, kept = 0, exp_fail = 0, map_fail = 0;
   std::lock_guard<std::mutex> lk(init_mu_);
   for (auto& kv : devs_) {
     if (kv.second->ipc) {
       kept += kv.second->ipc->kept_exports();
+      exp_fail += kv.second->ipc->zc_export_failures();
+      map_fail += kv.second->ipc->zc_map_failures();
       size_ref += kv.second->ipc->zc_size_refusals();
       full_ref += kv.second->ipc->zc_full_refusals();
     }
@@ -670,6 +672,8 @@ std::map<std::string, uint64_t> ProcessGroupMI355X::zc_counters() {
   out["zc_exchange_fallbacks"] = xchg_fallbacks;
   out["ipc_stale_maps"] = IpcComm::stale_mappings();
   out["ipc_kept_exports"] = kept;
+  out["zc_export_failures"] = exp_fail;
+  out["zc_map_failures"] = map_fail;
   return out;
 }
 

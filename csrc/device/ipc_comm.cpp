@@ -525,6 +525,7 @@ IpcComm::ZcRec IpcComm::zc_export(const void* p, size_t len, bool capturing) {
     e.base = static_cast<char*>(base);
     if (hipIpcGetMemHandle(&e.handle, base) != hipSuccess) {
       (void)hipGetLastError();  // e.g. a range the runtime refuses to export (ranks sharing a device)
+      ++export_failures_;
       return r;
     }
     // LRU eviction (never while capturing: importers could not drain their streams
@@ -669,6 +670,7 @@ bool IpcComm::zc_import(const std::vector<ZcRec>& all, const void* mine, bool al
       if (log_ >= 3) fprintf(stderr, "[pdcc r%d] ipc: open id %llu of rank %d\n", rank_, (unsigned long long)all[r].id, r);
       if (hipIpcOpenMemHandle(&m, all[r].handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !m) {
         (void)hipGetLastError();
+        ++map_failures_;
         if (!all[r].fresh)  // every rank mapped it when it was fresh: this cannot be agreed on any more
           throw std::runtime_error("pdcc: zero-copy IPC: re-mapping a confirmed peer buffer failed on rank " +
                                    std::to_string(rank_));

@@ -190,6 +190,9 @@ class IpcComm {
   uint64_t zc_full_refusals() const { return full_refusals_.load(); }
   // exports refused because the allocation's size has bit 31 set (see zc_export)
   uint64_t zc_size_refusals() const { return size_refusals_.load(); }
+  // exports the runtime refused (hipIpcGetMemHandle) / peer buffers this rank could not map
+  uint64_t zc_export_failures() const { return export_failures_.load(); }
+  uint64_t zc_map_failures() const { return map_failures_.load(); }
   // stale peer mappings the runtime handed back for fresh exports and that were re-opened
   // (process-wide; see open_handle in ipc_comm.cpp)
   static uint64_t stale_mappings();
@@ -284,6 +287,8 @@ class IpcComm {
   std::atomic<bool> peer_full_{false};      // some rank reported `full` in the last exchange
   std::atomic<uint64_t> full_refusals_{0};
   std::atomic<uint64_t> size_refusals_{0};
+  std::atomic<uint64_t> export_failures_{0};
+  std::atomic<uint64_t> map_failures_{0};
   bool size_guard_ = true;
   bool released_ = false;
   // Ranks sharing one GPU: a buffer this rank exported is never freed (outgrown staging, the group's

@@ -113,6 +113,7 @@ class _Pass:
         # this rank (the label is the outcome of the last call; the counter covers every call)
         want_zc = expect_engine is not None and "_zc" in expect_engine
         zc0 = zc_fallbacks(gb) if want_zc else 0
+        c0 = _zc_reasons(gb) if want_zc else {}
         try:
             ok = bool(fn())
         except Exception as e:  # a failing check must not stop the pass on this rank only
@@ -129,6 +130,9 @@ class _Pass:
             rec["want"] = expect_engine
         if want_zc:
             rec["zc_fallbacks"] = fb
+            if fb:  # why: the refusal counters that moved during the check
+                c1 = _zc_reasons(gb)
+                rec["zc_why"] = {k: c1[k] - c0.get(k, 0) for k in c1 if c1[k] != c0.get(k, 0)}
         if err:
             rec["error"] = err
         self.checks[name] = rec
@@ -140,6 +144,15 @@ class _Pass:
         return {"all_ok": not failed and not self.skipped, "passed": len(self.checks) - len(failed),
                 "failed": failed, "skipped": self.skipped, "elapsed_s": round(time.monotonic() - self.t0, 2),
                 "checks": self.checks}
+
+
+def _zc_reasons(gb) -> dict:
+    """The group's zero-copy refusal counters (size guard, full mapping list, exchange fallbacks)."""
+    if gb is None or not hasattr(gb, "zc_counters"):
+        return {}
+    c = gb.zc_counters()
+    return {k: int(c.get(k, 0)) for k in ("zc_size_refusals", "zc_full_refusals", "zc_exchange_fallbacks",
+                                          "zc_export_failures", "zc_map_failures")}
 
 
 def zc_fallbacks(gb) -> int:

@@ -22,8 +22,8 @@ def verdict(v):
         return "error: " + v["__error__"][:300]
     if isinstance(v, dict):
         if "all_ok" in v:
-            return "ok" if v["all_ok"] else "failed: " + ", ".join(k for k, c in v.get("checks", {}).items()
-                                                                     if not c.get("ok"))[:300]
+            return "ok" if v["all_ok"] else "failed: " + json.dumps(
+                {k: c for k, c in v.get("checks", {}).items() if not c.get("ok")})[:1500]
         bad = [k for k, x in v.items() if x is False]
         return "ok" if not bad else "failed: " + ", ".join(bad)[:300]
     if isinstance(v, list) and all(isinstance(x, bool) for x in v):
@@ -34,6 +34,8 @@ def verdict(v):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, nargs="*", default=[2, 4])
+    ap.add_argument("--only", nargs="*", default=None, help="phase keys to run (default: every one)")
+    ap.add_argument("--hwq", default="1", help="GPU_MAX_HW_QUEUES for 5+ ranks ('' = the runtime's default)")
     a = ap.parse_args()
     from pytorch_distributed_collective_communication_amd.parallel.spawn import launch
     from tests import _workers as W
@@ -41,9 +43,12 @@ def main():
 
     for w in a.world:
         d = tempfile.mkdtemp()
-        plan = [p for p in _plan(w, d) if p[3].get("PDCC_ALGO") != "rccl" and not p[0].startswith(NEEDS_DISTINCT)]
+        plan = [p for p in _plan(w, d) if p[3].get("PDCC_ALGO") != "rccl" and not p[0].startswith(NEEDS_DISTINCT)
+                and (a.only is None or p[0] in a.only)]
+        # (5+ ranks on one GPU: one hardware queue each, as the shared-GPU tests run them)
+        env = {"GPU_MAX_HW_QUEUES": a.hwq} if w >= 5 and a.hwq else {}
         res = launch(W.distinct_suite, w, args=("cuda", tuple(plan), d), bind_device=True, timeout_s=120,
-                     join_timeout_s=900)
+                     join_timeout_s=900, env=env)
         for key, *_ in plan:
             print(json.dumps({"world": w, "phase": key, "per_rank": [verdict(r[key]) for r in res]}), flush=True)
 

@@ -1653,7 +1653,7 @@ def coalesced_probe(rank, size, device="cpu", n=64, base=4096, timing=False):
     return res
 
 
-def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(10 << 20) // 4 + 64):
+def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(10 << 20) // 4 + 64, sync=False):
     """async zero-copy all_reduces over more allocations than the export cache holds,
     with NO barrier anywhere (evicted mappings can only be closed at safe points): the list of
     evicted-but-open mappings must stay bounded (a full rank refuses fresh exports / imports, those
@@ -1677,10 +1677,16 @@ def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(
         m = re.search(key + r"=(\d+)", b.describe())
         return int(m.group(1)) if m else -1
 
+    churn_algo = []
     for rnd in range(rounds):
         for i, t in enumerate(bufs):
             t.fill_(float(rank + i))
-            dist.all_reduce(t, async_op=True).wait()
+            if sync:  # synchronous calls, each finished on the host before the next (conformance's pattern)
+                dist.all_reduce(t)
+                torch.cuda.synchronize()
+                churn_algo.append(b.last_algo())
+            else:
+                dist.all_reduce(t, async_op=True).wait()
             hot.fill_(float(rank + 1))
             dist.all_reduce(hot, async_op=True).wait()
             hot_algo.append(b.last_algo())
@@ -1691,7 +1697,7 @@ def zc_churn_nobarrier_probe(rank, size, device="cuda", allocs=24, rounds=4, n=(
         closing.append(grab("zc_closing"))
         fast.append(grab("zx_fast"))
     return {"ok": ok, "closing": closing, "fast": fast, "refusals": grab("zc_full_refusals"),
-            "hot_algo": sorted(set(hot_algo[allocs:])), "desc": b.describe()}
+            "hot_algo": sorted(set(hot_algo[allocs:])), "churn_algo": sorted(set(churn_algo)), "desc": b.describe()}
 
 def async_grid_probe(rank, size, device="cuda", calls=6):
     """PDCC_IPC_ASYNC_GRID: async_op=True IPC launches run the capped grid (counted in
