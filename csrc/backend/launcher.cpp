@@ -74,6 +74,13 @@ void ProcessGroupMI355X::launcher_loop(DeviceState* dsp, IpcLauncher* lp) {
   }
 }
 
+bool ProcessGroupMI355X::launcher_idle(DeviceState& ds) {
+  if (!ds.launcher) return true;
+  IpcLauncher& L = *ds.launcher;
+  std::lock_guard<std::mutex> lk(L.mu);
+  return L.q.empty() && !L.busy;
+}
+
 void ProcessGroupMI355X::launcher_quiesce(DeviceState& ds) {
   if (!ds.launcher) return;
   IpcLauncher& L = *ds.launcher;
@@ -107,10 +114,11 @@ uint64_t ProcessGroupMI355X::ipc_gated(DeviceState& ds, const kern::IpcCall& cal
   // submitting thread, before this call's export: with every call gated (no inline exchange, no
   // barrier) the closing lists otherwise only grow, and at W = 8 (seven peers' entries per eviction)
   // a run of fresh buffers filled them within ~30 calls and every later fresh export was refused
-  // (staged; conformance's op checks, profiles/r6/plan_rehearsal_w8.jsonl). Every earlier call's
-  // exchange job is queued already, so the device synchronisation a close implies cannot wait on
-  // this thread.
-  if (ic.zc_closing() > 0) ic.reap_closing(false);
+  // (staged; conformance's op checks, profiles/r6/plan_rehearsal_w8_conformance_before.jsonl). Only
+  // while the launcher is idle: a close synchronises the device, and with no exchange job queued or
+  // running no kernel in flight waits on a host thread (and no mapping is being opened meanwhile) --
+  // the state an inline exchange closes in (design.md §3, "Evictions without a safe point").
+  if (ic.zc_closing() > 0 && launcher_idle(ds)) ic.reap_closing(false);
   const IpcComm::ZcRec mine = ic.zc_export(zbuf, zlen, false);
   hp_.lap(HostStage::ZC_EXPORT);
   const uint64_t t = ic.gate_reserve();

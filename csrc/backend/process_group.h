@@ -517,6 +517,7 @@ class ProcessGroupMI355X : public c10d::Backend {
   // thread's jobs and inline exchanges share it, one at a time, in issue order)
   host::ShmComm& exchange_channel(DeviceState& ds);
   static c10d::OpType op_type(Coll c);
+  bool launcher_idle(DeviceState& ds);  // no exchange job queued or running (non-blocking)
   void stop_launchers();
 
   // p2p on CPU runs on two background threads (so isend/irecv pairs never deadlock)
