@@ -57,7 +57,11 @@ def init_process(
     os.environ["WORLD_SIZE"] = str(size)
     os.environ.setdefault("LOCAL_RANK", str(rank))
     if bind_device and torch.cuda.device_count() > 0:
-        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count())
+        # PDCC_SPAWN_DEVICE=<i>: every rank on device i (ranks sharing one GPU on any box -- the
+        # shared-GPU tests); otherwise local rank r on device r (modulo the devices there are)
+        shared = os.environ.get("PDCC_SPAWN_DEVICE", "")
+        idx = int(shared) if shared else int(os.environ["LOCAL_RANK"])
+        torch.cuda.set_device(idx % torch.cuda.device_count())
     kw = {}
     if timeout_s is not None:
         kw["timeout"] = datetime.timedelta(seconds=timeout_s)

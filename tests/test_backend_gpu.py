@@ -17,7 +17,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _gpu_launch(fn, world, args=("cuda",), env=None, timeout_s=60):
-    e = {"PDCC_IPC_TIMEOUT_HINT": "1"}
+    # every rank on the first visible GPU, also on a multi-GPU box: these tests exercise ranks sharing
+    # one device (tests/test_multi_gpu.py holds the one-rank-per-GPU checks)
+    e = {"PDCC_SPAWN_DEVICE": "0"}
     if world >= 5:
         # every rank shares this one GPU: past the hardware queues the GPU maps at once (5+ processes
         # with a comm stream each) the hardware time-slices them and every IPC call waits out a
