@@ -27,12 +27,10 @@ namespace {
 // the first group's on the peer side.
 //
 // Every exported buffer also carries a random 64-bit nonce in its last 8 bytes, published with the
-// handle: the importer reads it back through the mapping it was given. Right after a group was
-// destroyed and the next one made, the runtime was seen handing a peer back the mapping of the
-// previous group's (freed) buffer for a fresh export -- the new group's flags and staging then lived
-// in stale memory on one side and its first 2-shot all-reduce returned wrong sums on a shared GPU
-// (tests/test_backend_gpu.py::test_distinct_suite_machinery_on_shared_gpu, profiles/r6/). A stale
-// mapping shows up as a wrong nonce: it is closed and opened again until the runtime has let go of it.
+// handle: the importer reads it back through the mapping it was given, so a mapping that does not show
+// the exporter's fresh buffer (a stale one the runtime handed back) is caught before any kernel uses it;
+// it is closed and opened again (`ipc_stale_maps`). Added while chasing wrong sums in re-made groups on a
+// shared GPU; none was ever seen -- the cause was elsewhere (release(), profiles/r6/regroup/README.md).
 constexpr size_t kNonceBytes = 64;  // reserved at the end of every exported buffer
 std::atomic<uint64_t> g_stale_maps{0};
 
@@ -265,12 +263,12 @@ IpcComm::~IpcComm() {
 }
 
 // Teardown order across the group: every rank closes its mappings of the peers' buffers, the ranks
-// meet, and only then does each free what it exported. Freeing an exported buffer while a peer still
-// had it mapped (ranks sharing one GPU, dmabuf IPC) left device memory that the next allocations on
-// both sides were handed at once: the next group's first bulk all-reduce on the shared GPU read zeros
-// in place of a fresh tensor's values (tests/_workers.py::regroup_probe, profiles/r6/regroup/).
-// Without the meeting (no deadline given, or a peer that never arrives) the exported buffers are kept
-// (a leak of the signal area and staging, never a free under a peer's mapping).
+// meet, and only then does each free what it exported -- never a free under a peer's mapping. Without
+// the meeting (no deadline given, or a peer that never arrives) the exported buffers are kept (a leak
+// of the signal area and staging). Ranks sharing one GPU never free them at all (keep_exports_): there,
+// a buffer a peer had mapped, once unmapped and freed -- in either order, with the meeting too -- came
+// back to both processes at once (the next group's fresh tensor zeroed by a peer's memset;
+// tests/_workers.py::regroup_probe / bulk_pre_diag, profiles/r6/regroup/README.md).
 void IpcComm::release(std::chrono::milliseconds deadline) {
   if (released_) return;
   released_ = true;
@@ -322,7 +320,7 @@ void IpcComm::release(std::chrono::milliseconds deadline) {
     if (my_flags_) parked_.push_back(reinterpret_cast<char*>(my_flags_));
     my_flags_ = nullptr;
     const bool met = !keep_exports_ && deadline.count() > 0 && store_barrier_for(store_, key_ + "/ipc_release", rank_, world_, deadline);
-    if (met && !keep_exports_) {
+    if (met) {
       for (char* q : parked_) dev_free(q);
     } else if (keep_exports_) {
       kept_exports_ += parked_.size();  // ranks sharing one GPU: see keep_exports_
