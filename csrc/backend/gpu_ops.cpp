@@ -19,6 +19,12 @@ namespace pdcc {
 
 using namespace gpu;
 
+// a call whose IPC engine is an LL kernel (whatever engine the autotuner then picks, every one of them
+// takes buffers at any alignment: LL, RCCL, the host path)
+bool ProcessGroupMI355X::ll_call(const DeviceState& ds, size_t bytes) const {
+  return ds.ipc_ok && ds.ll_ok && bytes_in_ll_range(bytes);
+}
+
 bool ProcessGroupMI355X::bytes_in_ll_range(size_t bytes) const {
   return bytes > 0 && bytes <= std::min(cfg_.ipc_ll_max, kern::kLLMaxBytes);
 }
@@ -925,10 +931,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allgather(std::vector<at:
   }
   DeviceState& ds = dev_state(in);
   const Algo a0 = choose(cname, bytes, ds, ds.rccl_ok, ds.ipc_ok);
-  at::Tensor wi = prep_in(in);
+  const bool any_align = ll_call(ds, bytes);  // (see prep_in)
+  at::Tensor wi = prep_in(in, any_align);
   std::vector<at::Tensor> wo;
   if (receiver)
-    for (auto& o : outs) wo.push_back(prep_out(o));
+    for (auto& o : outs) wo.push_back(prep_out(o, any_align));
   // the layout is part of the key (RCCL takes a different path for a flat output);
   // on gather only the root has outputs, so the key cannot depend on them there
   const bool flat = !rooted && is_flat(wo, bytes);
@@ -1001,10 +1008,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_scatter(at::Tensor& out, 
   }
   DeviceState& ds = dev_state(out);
   const Algo a0 = choose(Coll::SCATTER, bytes, ds, ds.rccl_ok, ds.ipc_ok);
+  const bool any_align = ll_call(ds, bytes);  // (see prep_in)
   std::vector<at::Tensor> wi;
   if (rank_ == root)
-    for (auto& i : ins) wi.push_back(prep_in(i));
-  at::Tensor wo = prep_out(out);
+    for (auto& i : ins) wi.push_back(prep_in(i, any_align));
+  at::Tensor wo = prep_out(out, any_align);
   const Algo a = decide(Coll::SCATTER, -1, -1, bytes, ds, a0, ds.rccl_ok, ds.ipc_ok,
                         [&](const TuneKey& key, const std::vector<Algo>& cands) {
     const int64_t n = sample_numel(wo.numel(), wo.element_size(), cfg_.autotune_sample, size_);
@@ -1058,9 +1066,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_reduce_scatter(at::Tensor
   const bool nok = nccl_dtype(out.scalar_type(), nd) && nccl_op(op, out.scalar_type(), no);
   const bool rccl_can = ds.rccl_ok && nok, ipc_can = ds.ipc_ok && kok;
   const Algo a0 = choose(Coll::REDUCE_SCATTER, bytes, ds, rccl_can, ipc_can);
+  const bool any_align = ll_call(ds, bytes);  // (see prep_in)
   std::vector<at::Tensor> wi;
-  for (auto& i : ins) wi.push_back(prep_in(i));
-  at::Tensor wo = prep_out(out);
+  for (auto& i : ins) wi.push_back(prep_in(i, any_align));
+  at::Tensor wo = prep_out(out, any_align);
   const Algo a = decide(Coll::REDUCE_SCATTER, (int)out.scalar_type(), (int)op, bytes, ds, a0, rccl_can, ipc_can,
                         [&](const TuneKey& key, const std::vector<Algo>& cands) {
     const int64_t n = sample_numel(wo.numel(), wo.element_size(), cfg_.autotune_sample, size_);
@@ -1125,9 +1134,10 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_alltoall(std::vector<at::
   const size_t chunk = ins[0].nbytes();
   const bool ipc_can = ds.ipc_ok && equal;
   const Algo a0 = choose(Coll::ALLTOALL, equal ? chunk : SIZE_MAX, ds, ds.rccl_ok, ipc_can);
+  const bool any_align = equal && ll_call(ds, chunk);  // (see prep_in)
   std::vector<at::Tensor> wi, wo;
-  for (auto& i : ins) wi.push_back(prep_in(i));
-  for (auto& o : outs) wo.push_back(prep_out(o));
+  for (auto& i : ins) wi.push_back(prep_in(i, any_align));
+  for (auto& o : outs) wo.push_back(prep_out(o, any_align));
   const bool flat = equal && is_flat(wi, chunk) && is_flat(wo, chunk);
   const Algo a = !equal ? a0 : decide(Coll::ALLTOALL, -1, flat ? kLayoutFlat : kLayoutList, chunk, ds, a0,
                                       ds.rccl_ok, ipc_can, [&](const TuneKey& key, const std::vector<Algo>& cands) {

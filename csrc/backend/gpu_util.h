@@ -100,16 +100,19 @@ constexpr int kLayoutFlat = 100, kLayoutList = 101;
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// input used in place: contiguous + 16-B aligned, else a copy (on the current stream)
-inline at::Tensor prep_in(const at::Tensor& t) {
-  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
+// input used in place: contiguous + 16-B aligned, else a copy (on the current stream). `any_align`:
+// a call every engine of which takes any alignment -- the LL kernels (byte-wise where a line is not
+// 8-B aligned), RCCL, the host path -- so a view of one flat tensor at a small offset (a 4 B chunk of
+// all_gather_into_tensor's output) is used in place instead of costing a copy kernel per chunk
+inline at::Tensor prep_in(const at::Tensor& t, bool any_align = false) {
+  if (t.is_contiguous() && (any_align || aligned16(t.data_ptr()))) return t;
   at::Tensor c = at::empty_like(t, at::MemoryFormat::Contiguous);
   c.copy_(t);
   return c;
 }
-// pure output: contiguous + aligned, else fresh storage (copied back afterwards)
-inline at::Tensor prep_out(const at::Tensor& t) {
-  if (t.is_contiguous() && aligned16(t.data_ptr())) return t;
+// pure output: contiguous + aligned (or `any_align`, as above), else fresh storage (copied back afterwards)
+inline at::Tensor prep_out(const at::Tensor& t, bool any_align = false) {
+  if (t.is_contiguous() && (any_align || aligned16(t.data_ptr()))) return t;
   return at::empty_like(t, at::MemoryFormat::Contiguous);
 }
 

@@ -624,6 +624,7 @@ class ProcessGroupMI355X : public c10d::Backend {
  private:
   // payload size the LL protocol takes (PDCC_IPC_LL_MAX, at most kern::kLLMaxBytes)
   bool bytes_in_ll_range(size_t bytes) const;
+  bool ll_call(const DeviceState& ds, size_t bytes) const;
 
  private:
   std::vector<c10::intrusive_ptr<WorkMI355X>> coalesced_cpu_;

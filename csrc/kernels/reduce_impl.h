@@ -716,8 +716,14 @@ __device__ __forceinline__ uint64_t* ll_slot(uint32_t* sig, uint32_t parity, int
                                      ((size_t)parity * kern::kMaxRanks + (size_t)src) * kern::kLLSlotBytes);
 }
 
+// (byte-wise where the line is short or not 8-B aligned: views of one flat tensor at 4 B offsets are
+// used in place, prep_in's any_align)
+__device__ __forceinline__ bool ll_whole(const char* p, size_t off, size_t nbytes) {
+  return off + 8 <= nbytes && (reinterpret_cast<uintptr_t>(p + off) & 7u) == 0;
+}
+
 __device__ __forceinline__ uint2 ll_load(const char* p, size_t off, size_t nbytes) {
-  if (off + 8 <= nbytes) return *reinterpret_cast<const uint2*>(p + off);
+  if (ll_whole(p, off, nbytes)) return *reinterpret_cast<const uint2*>(p + off);
   uint32_t w[2] = {0u, 0u};
 #pragma unroll
   for (int k = 0; k < 8; ++k)
@@ -726,7 +732,7 @@ __device__ __forceinline__ uint2 ll_load(const char* p, size_t off, size_t nbyte
 }
 
 __device__ __forceinline__ void ll_store(char* p, size_t off, size_t nbytes, uint32_t x, uint32_t y) {
-  if (off + 8 <= nbytes) {
+  if (ll_whole(p, off, nbytes)) {
     *reinterpret_cast<uint2*>(p + off) = make_uint2(x, y);
     return;
   }

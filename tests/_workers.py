@@ -2158,3 +2158,53 @@ def bulk_pre_diag(rank, size, device="cuda", n=3_000_017):
     return [len(bad), pre, be.native_backend(None, "cuda").last_algo(), i,
             (float(got[i]), float(want[i])) if i >= 0 else None]
 
+
+
+def ll_unaligned_probe(rank, size, device="cuda"):
+    """LL collectives on views of one flat tensor at 4-byte offsets (not 16-B / 8-B aligned), used in place
+    (prep_in any_align, byte-wise LL lines): all_gather_into_tensor, reduce_scatter_tensor, all_to_all_single,
+    scatter and gather through list views of one buffer, for 1, 3 and 1001 fp32 per rank -- exact against
+    the expected values; plus the engine label."""
+    import torch
+    import torch.distributed as dist
+
+    from pytorch_distributed_collective_communication_amd.parallel import backend as be
+
+    d = _dev(device)
+    b = be.native_backend(None, "cuda")
+    ok, algos = {}, set()
+    for n in (1, 3, 1001):
+        src = torch.arange(n, device=d, dtype=torch.float32) + 1000 * rank
+        flat = torch.full((n * size,), -1.0, device=d)
+        dist.all_gather_into_tensor(flat, src)
+        algos.add(b.last_algo())
+        want = torch.cat([torch.arange(n, device=d, dtype=torch.float32) + 1000 * r for r in range(size)])
+        ok[f"ag/{n}"] = bool(torch.equal(flat, want))
+        # an offset input view too: element 1.. of a bigger buffer
+        big = torch.zeros(n + 1, device=d)
+        big[1:] = src
+        flat2 = torch.full((n * size + 1,), -1.0, device=d)[1:]
+        dist.all_gather_into_tensor(flat2, big[1:])
+        ok[f"ag_offset/{n}"] = bool(torch.equal(flat2, want))
+        inp = torch.arange(n * size, device=d, dtype=torch.float32) + rank
+        out = torch.full((n,), -1.0, device=d)
+        dist.reduce_scatter_tensor(out, inp)
+        algos.add(b.last_algo())
+        rs_want = (torch.arange(n * size, device=d, dtype=torch.float32) * size + size * (size - 1) / 2)[rank * n:(rank + 1) * n]
+        ok[f"rs/{n}"] = bool(torch.equal(out, rs_want))
+        a_in = torch.arange(n * size, device=d, dtype=torch.float32) + 100000 * rank
+        a_out = torch.full((n * size,), -1.0, device=d)
+        dist.all_to_all_single(a_out, a_in)
+        algos.add(b.last_algo())
+        a_want = torch.cat([torch.arange(rank * n, (rank + 1) * n, device=d, dtype=torch.float32) + 100000 * q
+                            for q in range(size)])
+        ok[f"a2a/{n}"] = bool(torch.equal(a_out, a_want))
+        sbuf = torch.arange(n * size, device=d, dtype=torch.float32) + 7
+        s_out = torch.full((n,), -1.0, device=d)
+        dist.scatter(s_out, scatter_list=list(sbuf.split(n)) if rank == 0 else None, src=0)
+        ok[f"scatter/{n}"] = bool(torch.equal(s_out, sbuf[rank * n:(rank + 1) * n]))
+        gbuf = torch.full((n * size,), -1.0, device=d)
+        dist.gather(src, gather_list=list(gbuf.split(n)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            ok[f"gather/{n}"] = bool(torch.equal(gbuf, want))
+    return {"ok": ok, "algos": sorted(algos)}

@@ -761,3 +761,15 @@ def test_distinct_suite_machinery_on_shared_gpu(tmp_path):
     ref = W.zero_reference("adam")
     for r in res:
         torch.testing.assert_close(torch.tensor(r["zero_train"][0]), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ll_collectives_on_views_at_4_byte_offsets(world):
+    # round 6: an all_gather_into_tensor of 4 B per rank cost a copy kernel per output chunk (views at
+    # 4 B offsets failed the 16-B alignment check): 31 us per call at W = 4 against 12 for a list output
+    # (scripts/ag_small_probe.py). LL calls now take every buffer in place at any alignment -- checked
+    # exact here for every LL kind with 1, 3 and 1001 fp32 per rank
+    for r in _gpu_launch(W.ll_unaligned_probe, world, env={"PDCC_ALGO": "ipc"}):
+        assert all(r["ok"].values()), r
+        assert r["algos"] == ["ipc_ll"], r
+
