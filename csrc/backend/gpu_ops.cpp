@@ -808,7 +808,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_allreduce(at::Tensor& t, 
   const bool nok = nccl_dtype(t.scalar_type(), nd) && nccl_op(op, t.scalar_type(), no);
   const bool rccl_can = ds.rccl_ok && nok, ipc_can = ds.ipc_ok && kok;
   const Algo a0 = choose(cname, bytes, ds, rccl_can, ipc_can);
-  at::Tensor w = prep_in(t);
+  at::Tensor w = prep_in(t, ipc_can && ll_call(ds, bytes));  // (an LL call: any alignment, see prep_in)
   const Algo a = decide(cname, (int)t.scalar_type(), (int)op, bytes, ds, a0, rccl_can, ipc_can,
                         [&](const TuneKey& key, const std::vector<Algo>& cands) {
     const int64_t n = sample_numel(w.numel(), w.element_size(), cfg_.autotune_sample);
@@ -874,7 +874,7 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::gpu_broadcast(at::Tensor& t, 
   }
   DeviceState& ds = dev_state(t);
   const Algo a0 = choose(Coll::BROADCAST, bytes, ds, ds.rccl_ok, ds.ipc_ok);
-  at::Tensor w = prep_in(t);
+  at::Tensor w = prep_in(t, ll_call(ds, bytes));  // (an LL call: any alignment, see prep_in)
   const Algo a = decide(Coll::BROADCAST, -1, -1, bytes, ds, a0, ds.rccl_ok, ds.ipc_ok,
                         [&](const TuneKey& key, const std::vector<Algo>& cands) {
     const int64_t n = sample_numel(w.numel(), w.element_size(), cfg_.autotune_sample);

@@ -2207,4 +2207,20 @@ def ll_unaligned_probe(rank, size, device="cuda"):
         dist.gather(src, gather_list=list(gbuf.split(n)) if rank == 0 else None, dst=0)
         if rank == 0:
             ok[f"gather/{n}"] = bool(torch.equal(gbuf, want))
+        # in-place collectives on a view at a 4-byte offset: all_reduce, reduce, broadcast
+        buf = torch.full((n + 1,), -5.0, device=d)
+        v = buf[1:]
+        v.copy_(torch.arange(n, device=d, dtype=torch.float32) + rank)
+        dist.all_reduce(v)
+        algos.add(b.last_algo())
+        ar_want = torch.arange(n, device=d, dtype=torch.float32) * size + size * (size - 1) / 2
+        ok[f"ar_offset/{n}"] = bool(torch.equal(v, ar_want)) and float(buf[0]) == -5.0
+        v.copy_(torch.arange(n, device=d, dtype=torch.float32) + rank)
+        dist.reduce(v, dst=0)
+        if rank == 0:
+            ok[f"reduce_offset/{n}"] = bool(torch.equal(v, ar_want)) and float(buf[0]) == -5.0
+        v.copy_(torch.arange(n, device=d, dtype=torch.float32) * (3 if rank == 0 else 0))
+        dist.broadcast(v, src=0)
+        ok[f"bcast_offset/{n}"] = bool(torch.equal(v, torch.arange(n, device=d, dtype=torch.float32) * 3)) and \
+            float(buf[0]) == -5.0
     return {"ok": ok, "algos": sorted(algos)}
