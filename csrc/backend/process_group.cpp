@@ -510,6 +510,9 @@ void ProcessGroupMI355X::maybe_inject_fault() {
 }
 
 void ProcessGroupMI355X::before_op(Coll c, const std::vector<at::Tensor>& ts, int root) {
+  // (the stage profiler's clock: allreduce() starts it on entry; every other collective here, so its
+  // first stage is not measured from the previous op)
+  if (c != Coll::ALLREDUCE) hp_.start();
   if (health_->poisoned.load())
     throw std::runtime_error("pdcc: process group is in an error state: " + health_->message());
   ++op_seq_;
