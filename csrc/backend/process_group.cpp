@@ -1077,9 +1077,11 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_allgather_base(at::Tensor& o
               output.numel(), " elements, expected ", input.numel() * size_);
   TORCH_CHECK(output.scalar_type() == input.scalar_type(), "ProcessGroupMI355X::_allgather_base: dtype mismatch");
   TORCH_CHECK(output.is_contiguous(), "ProcessGroupMI355X::_allgather_base: output must be contiguous");
+  // one 1-D view per rank (only numel, dtype and device are checked; the engines need the pointers):
+  // one split instead of a narrow + view per rank keeps a small call's host time down
   std::vector<std::vector<at::Tensor>> outs(1);
-  auto flat = output.view({-1});
-  for (int r = 0; r < size_; ++r) outs[0].push_back(flat.narrow(0, r * input.numel(), input.numel()).view(input.sizes()));
+  outs[0] = input.numel() > 0 ? output.view({-1}).split(input.numel())
+                              : std::vector<at::Tensor>((size_t)size_, output.view({-1}));
   std::vector<at::Tensor> ins{input};
   return allgather(outs, ins, opts);
 }
@@ -1180,9 +1182,9 @@ c10::intrusive_ptr<c10d::Work> ProcessGroupMI355X::_reduce_scatter_base(at::Tens
   TORCH_CHECK(input.numel() == output.numel() * size_, "ProcessGroupMI355X::_reduce_scatter_base: input has ",
               input.numel(), " elements, expected ", output.numel() * size_);
   TORCH_CHECK(input.is_contiguous(), "ProcessGroupMI355X::_reduce_scatter_base: input must be contiguous");
-  std::vector<std::vector<at::Tensor>> ins(1);
-  auto flat = input.view({-1});
-  for (int r = 0; r < size_; ++r) ins[0].push_back(flat.narrow(0, r * output.numel(), output.numel()).view(output.sizes()));
+  std::vector<std::vector<at::Tensor>> ins(1);  // (one split, as in _allgather_base)
+  ins[0] = output.numel() > 0 ? input.view({-1}).split(output.numel())
+                              : std::vector<at::Tensor>((size_t)size_, input.view({-1}));
   std::vector<at::Tensor> outs{output};
   return reduce_scatter(outs, ins, opts);
 }
